@@ -1,0 +1,143 @@
+"""ctypes binding of libgpx.so (include/gpx.h).
+
+This is the only place Python touches the native library.  The library is built in-tree
+(``bayesianoptimizer_amd/lib/libgpx.so``, see ``__graft_entry__.build``); if it is missing the import of
+the engine fails loudly — there is no CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from ctypes import POINTER, c_char_p, c_double, c_int32, c_int64, c_size_t, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GPX_LIB", os.path.join(_HERE, "lib", "libgpx.so"))
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gpx.h")
+
+GPX_MAX_DIM = 32
+GPX_MAX_RHS = 8
+GPX_TILE = 128
+
+GPX_OK, GPX_NOT_PD, GPX_INVALID_ARG, GPX_HIP_ERROR, GPX_RCCL_ERROR = 0, 1, 2, 3, 4
+STATUS_NAMES = {0: "OK", 1: "NOT_PD", 2: "INVALID_ARG", 3: "HIP_ERROR", 4: "RCCL_ERROR"}
+
+KERNEL_RBF, KERNEL_MATERN52, KERNEL_SCALE_LINEAR_MATERN52 = 0, 1, 2
+ACQ_EI, ACQ_LOGEI, ACQ_UCB, ACQ_VARIANCE = 0, 1, 2, 3
+TIMERS = {"gram": 0, "potrf": 1, "trtri": 2, "alpha": 3, "kstar": 4, "trmm": 5, "acq": 6}
+
+
+class GPXLibraryError(RuntimeError):
+    """libgpx.so is missing or failed to load (the HIP path is required; there is no fallback)."""
+
+
+class GPXError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"gpx {STATUS_NAMES.get(status, status)}: {message}")
+        self.status = status
+
+
+class NotPositiveDefiniteError(GPXError):
+    """Raised when the Cholesky of K(X,X)+noise*I fails; ``pivot`` is 0-based (reference retries with
+    a larger jitter, optimization/Bayesian6.py:481-488)."""
+
+    def __init__(self, pivot: int, message: str = ""):
+        super().__init__(GPX_NOT_PD, message or f"matrix not positive definite at pivot {pivot}")
+        self.pivot = pivot
+
+
+class KernelParamsC(ctypes.Structure):
+    _fields_ = [
+        ("kind", c_int32),
+        ("d", c_int32),
+        ("lengthscale", c_double * GPX_MAX_DIM),
+        ("linear_variance", c_double * GPX_MAX_DIM),
+        ("outputscale", c_double),
+        ("noise", c_double),
+        ("jitter", c_double),
+        ("const_mean", c_double),
+    ]
+
+
+class AcqParamsC(ctypes.Structure):
+    _fields_ = [
+        ("kind", c_int32),
+        ("reserved", c_int32),
+        ("best_f", c_double),
+        ("beta", c_double),
+        ("y_mean", c_double),
+        ("y_scale", c_double),
+    ]
+
+
+_h = c_void_p
+_p = c_void_p  # device pointers
+_PROTOS = {
+    "gpx_version": (c_char_p, []),
+    "gpx_create": (c_int32, [c_int32, POINTER(c_void_p)]),
+    "gpx_destroy": (c_int32, [_h]),
+    "gpx_set_stream": (c_int32, [_h, c_void_p]),
+    "gpx_last_error": (c_char_p, [_h]),
+    "gpx_padded_n": (c_int64, [c_int64]),
+    "gpx_gram_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64]),
+    "gpx_potrf_f64": (c_int32, [_h, c_int64, _p, c_int64, _p, _p]),
+    "gpx_trtri_workspace_size": (c_int32, [c_int64, POINTER(c_size_t)]),
+    "gpx_trtri_f64": (c_int32, [_h, c_int64, _p, c_int64, _p, _p, c_int64, _p, c_size_t]),
+    "gpx_alpha_workspace_size": (c_int32, [c_int64, c_int64, POINTER(c_size_t)]),
+    "gpx_alpha_f64": (c_int32, [_h, c_int64, _p, c_int64, _p, c_int64, c_int64, c_double, _p, _p, c_size_t]),
+    "gpx_fit_workspace_size": (c_int32, [c_int64, c_int64, POINTER(c_size_t)]),
+    "gpx_fit_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, c_int64, _p, c_int64,
+                              _p, _p, c_int64, _p, _p, _p, c_size_t]),
+    "gpx_fit_f64_sync": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, c_int64, _p,
+                                   c_int64, _p, _p, c_int64, _p, _p, _p, c_size_t, POINTER(c_int32)]),
+    "gpx_sweep_workspace_size": (c_int32, [c_int64, c_int64, c_int64, POINTER(c_size_t)]),
+    "gpx_posterior_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, _p, c_int64,
+                                    _p, c_int64, c_int64, POINTER(c_double), POINTER(c_double), _p, c_int64, _p,
+                                    _p, c_size_t]),
+    "gpx_acquire_argmax_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, _p, _p,
+                                         c_int64, c_int64, POINTER(AcqParamsC), c_int64, _p, _p, _p, _p,
+                                         c_size_t]),
+    "gpx_argmax_combine_f64": (c_int32, [_h, _p, _p, c_int64, _p, _p]),
+    "gpx_timing_enable": (c_int32, [_h, c_int32]),
+    "gpx_timing_reset": (c_int32, [_h]),
+    "gpx_timing_query": (c_int32, [_h, c_int32, POINTER(c_double), POINTER(c_int64)]),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libgpx.so once; raise GPXLibraryError (never fall back) when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GPXLibraryError(
+            f"libgpx.so not found at {LIB_PATH}; build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C bayesianoptimizer_amd/csrc` (hipcc --offload-arch=gfx950)")
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on the ROCm runtime being present
+        raise GPXLibraryError(f"failed to load {LIB_PATH}: {e}") from e
+    for name, (res, args) in _PROTOS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def header_symbols(path: str = HEADER_PATH):
+    """Names of every function declared in include/gpx.h (used by the ABI test)."""
+    text = open(path).read()
+    return sorted(set(re.findall(r"\b(gpx_[a-z0-9_]+)\s*\(", text)))
+
+
+def check(status: int, handle=None):
+    if status == GPX_OK:
+        return
+    msg = ""
+    if handle is not None and _lib is not None:
+        raw = _lib.gpx_last_error(handle)
+        msg = raw.decode() if raw else ""
+    raise GPXError(status, msg)

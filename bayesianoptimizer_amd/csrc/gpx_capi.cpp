@@ -1,0 +1,431 @@
+// The C ABI of libgpx.so (include/gpx.h): argument validation, workspace carving, chunk loop and timers.
+// Every exported symbol is extern "C" with plain pointers; no torch types cross this boundary.
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include "gpx_internal.h"
+
+using gpx::Context;
+
+namespace {
+
+constexpr const char* kVersion = "gpx 0.1.0 (gfx950, fp64 MFMA)";
+
+gpx_status fail(Context* c, gpx_status st, const std::string& msg) {
+  if (c) c->last_error = msg;
+  return st;
+}
+
+gpx_status hip_check(Context* c, hipError_t e, const char* where) {
+  if (e == hipSuccess) return GPX_OK;
+  return fail(c, GPX_HIP_ERROR, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+gpx_status use_device(Context* c) {
+  int cur = -1;
+  hipError_t e = hipGetDevice(&cur);
+  if (e != hipSuccess) return hip_check(c, e, "hipGetDevice");
+  if (cur != c->device) return hip_check(c, hipSetDevice(c->device), "hipSetDevice");
+  return GPX_OK;
+}
+
+int64_t padded(int64_t n) { return ((n + GPX_TILE - 1) / GPX_TILE) * GPX_TILE; }
+
+gpx_status check_params(Context* c, const gpx_kernel_params* p) {
+  if (!p) return fail(c, GPX_INVALID_ARG, "kernel params pointer is NULL");
+  if (p->kind < GPX_KERNEL_RBF || p->kind > GPX_KERNEL_SCALE_LINEAR_MATERN52)
+    return fail(c, GPX_INVALID_ARG, "unknown kernel kind " + std::to_string(p->kind));
+  if (p->d < 1 || p->d > GPX_MAX_DIM)
+    return fail(c, GPX_INVALID_ARG, "input dimension d=" + std::to_string(p->d) + " outside [1, 32]");
+  for (int k = 0; k < p->d; ++k)
+    if (!(p->lengthscale[k] > 0.0) || !std::isfinite(p->lengthscale[k]))
+      return fail(c, GPX_INVALID_ARG, "lengthscale[" + std::to_string(k) + "] must be positive and finite");
+  if (!(p->outputscale >= 0.0) || !(p->noise >= 0.0) || !(p->jitter >= 0.0))
+    return fail(c, GPX_INVALID_ARG, "outputscale/noise/jitter must be non-negative");
+  return GPX_OK;
+}
+
+gpx_status check_n(Context* c, int64_t n) {
+  if (n < 1 || n > (int64_t)1 << 20) return fail(c, GPX_INVALID_ARG, "n must be in [1, 2^20]");
+  return GPX_OK;
+}
+
+gpx_status check_ld(Context* c, int64_t ld, int64_t minimum, const char* name, bool even) {
+  if (ld < minimum) return fail(c, GPX_INVALID_ARG, std::string(name) + " leading dimension too small");
+  if (even && (ld & 1)) return fail(c, GPX_INVALID_ARG, std::string(name) + " leading dimension must be even");
+  return GPX_OK;
+}
+
+#define GPX_TRY(expr)               \
+  do {                              \
+    gpx_status _st = (expr);        \
+    if (_st != GPX_OK) return _st;  \
+  } while (0)
+
+#define GPX_NONNULL(c, ptr) \
+  do { if (!(ptr)) return fail((c), GPX_INVALID_ARG, #ptr " is NULL"); } while (0)
+
+size_t trtri_ws(int64_t npad) { return (size_t)npad * npad / 4 * 8 + 256; }
+size_t alpha_ws(int64_t npad, int64_t nrhs) { return ((size_t)(npad / 128) + 1) * npad * nrhs * 8 + 512; }
+
+double* align256(void* p) {
+  uintptr_t u = reinterpret_cast<uintptr_t>(p);
+  u = (u + 255) & ~(uintptr_t)255;
+  return reinterpret_cast<double*>(u);
+}
+
+}  // namespace
+
+namespace gpx {
+
+LaunchTimer::LaunchTimer(Context* ctx, int t) : c(ctx), timer(t) {
+  if (!(c->timing_mask & (1 << t))) return;
+  auto take = [&]() {
+    hipEvent_t ev;
+    if (!c->free_events.empty()) {
+      ev = c->free_events.back();
+      c->free_events.pop_back();
+    } else if (hipEventCreate(&ev) != hipSuccess) {
+      return (hipEvent_t) nullptr;
+    }
+    return ev;
+  };
+  s = take();
+  e = take();
+  if (s) (void)hipEventRecord(s, c->stream);
+}
+
+LaunchTimer::~LaunchTimer() {
+  if (!s || !e) return;
+  (void)hipEventRecord(e, c->stream);
+  c->pending.push_back({timer, s, e});
+}
+
+}  // namespace gpx
+
+extern "C" {
+
+const char* gpx_version(void) { return kVersion; }
+
+int64_t gpx_padded_n(int64_t n) { return padded(n); }
+
+gpx_status gpx_create(int32_t device, gpx_handle* out) {
+  if (!out) return GPX_INVALID_ARG;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return GPX_HIP_ERROR;
+  if (device < 0 || device >= count) return GPX_INVALID_ARG;
+  Context* c = new (std::nothrow) Context();
+  if (!c) return GPX_HIP_ERROR;
+  c->device = device;
+  if (use_device(c) != GPX_OK) {
+    delete c;
+    return GPX_HIP_ERROR;
+  }
+  *out = reinterpret_cast<gpx_handle>(c);
+  return GPX_OK;
+}
+
+gpx_status gpx_destroy(gpx_handle h) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& pt : c->pending) {
+    (void)hipEventDestroy(pt.start);
+    (void)hipEventDestroy(pt.stop);
+  }
+  for (auto ev : c->free_events) (void)hipEventDestroy(ev);
+  delete c;
+  return GPX_OK;
+}
+
+gpx_status gpx_set_stream(gpx_handle h, void* stream) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  c->stream = reinterpret_cast<hipStream_t>(stream);
+  return GPX_OK;
+}
+
+const char* gpx_last_error(gpx_handle h) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return "invalid handle";
+  return c->last_error.c_str();
+}
+
+gpx_status gpx_gram_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                        double* K, int64_t ldk) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_TRY(check_params(c, p));
+  GPX_TRY(check_n(c, n));
+  GPX_NONNULL(c, X);
+  GPX_NONNULL(c, K);
+  const int64_t npad = padded(n);
+  GPX_TRY(check_ld(c, ldx, p->d, "X", false));
+  GPX_TRY(check_ld(c, ldk, npad, "K", true));
+  GPX_TRY(use_device(c));
+  return hip_check(c, gpx::launch_gram(c, *p, (int)n, (int)npad, X, ldx, K, ldk), "gram");
+}
+
+gpx_status gpx_potrf_f64(gpx_handle h, int64_t n, double* A, int64_t lda, double* Dinv, int32_t* info) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_TRY(check_n(c, n));
+  GPX_NONNULL(c, A);
+  GPX_NONNULL(c, Dinv);
+  GPX_NONNULL(c, info);
+  const int64_t npad = padded(n);
+  GPX_TRY(check_ld(c, lda, npad, "A", true));
+  GPX_TRY(use_device(c));
+  GPX_TRY(hip_check(c, hipMemsetAsync(info, 0, sizeof(int32_t), c->stream), "memset info"));
+  return hip_check(c, gpx::launch_potrf(c, (int)npad, A, lda, Dinv, info), "potrf");
+}
+
+gpx_status gpx_trtri_workspace_size(int64_t n, size_t* bytes) {
+  if (!bytes || n < 1) return GPX_INVALID_ARG;
+  *bytes = trtri_ws(padded(n));
+  return GPX_OK;
+}
+
+gpx_status gpx_trtri_f64(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv, double* W,
+                         int64_t ldw, void* ws, size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_TRY(check_n(c, n));
+  GPX_NONNULL(c, L);
+  GPX_NONNULL(c, Dinv);
+  GPX_NONNULL(c, W);
+  GPX_NONNULL(c, ws);
+  const int64_t npad = padded(n);
+  GPX_TRY(check_ld(c, ldl, npad, "L", true));
+  GPX_TRY(check_ld(c, ldw, npad, "W", true));
+  if (ws_bytes < trtri_ws(npad)) return fail(c, GPX_INVALID_ARG, "trtri workspace too small");
+  GPX_TRY(use_device(c));
+  return hip_check(c, gpx::launch_trtri(c, (int)npad, L, ldl, Dinv, W, ldw, align256(ws)), "trtri");
+}
+
+gpx_status gpx_alpha_workspace_size(int64_t n, int64_t nrhs, size_t* bytes) {
+  if (!bytes || n < 1 || nrhs < 1 || nrhs > GPX_MAX_RHS) return GPX_INVALID_ARG;
+  *bytes = alpha_ws(padded(n), nrhs);
+  return GPX_OK;
+}
+
+gpx_status gpx_alpha_f64(gpx_handle h, int64_t n, const double* W, int64_t ldw, const double* Y, int64_t ldy,
+                         int64_t nrhs, double const_mean, double* alpha, void* ws, size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_TRY(check_n(c, n));
+  if (nrhs < 1 || nrhs > GPX_MAX_RHS) return fail(c, GPX_INVALID_ARG, "nrhs must be in [1, 8]");
+  GPX_NONNULL(c, W);
+  GPX_NONNULL(c, Y);
+  GPX_NONNULL(c, alpha);
+  GPX_NONNULL(c, ws);
+  const int64_t npad = padded(n);
+  GPX_TRY(check_ld(c, ldw, npad, "W", true));
+  GPX_TRY(check_ld(c, ldy, nrhs, "Y", false));
+  if (ws_bytes < alpha_ws(npad, nrhs)) return fail(c, GPX_INVALID_ARG, "alpha workspace too small");
+  GPX_TRY(use_device(c));
+  double* zpart = align256(ws);
+  double* z = zpart + (size_t)(npad / 128) * npad * nrhs;
+  return hip_check(c, gpx::launch_alpha(c, (int)n, (int)npad, W, ldw, Y, ldy, (int)nrhs, const_mean, alpha, zpart, z),
+                   "alpha");
+}
+
+gpx_status gpx_fit_workspace_size(int64_t n, int64_t nrhs, size_t* bytes) {
+  if (!bytes || n < 1 || nrhs < 1 || nrhs > GPX_MAX_RHS) return GPX_INVALID_ARG;
+  const int64_t npad = padded(n);
+  size_t a = trtri_ws(npad), b = alpha_ws(npad, nrhs);
+  *bytes = a > b ? a : b;
+  return GPX_OK;
+}
+
+gpx_status gpx_fit_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                       const double* Y, int64_t ldy, int64_t nrhs, double* K, int64_t ldk, double* Dinv, double* W,
+                       int64_t ldw, double* alpha, int32_t* info, void* ws, size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  size_t need = 0;
+  if (gpx_fit_workspace_size(n, nrhs, &need) != GPX_OK)
+    return fail(c, GPX_INVALID_ARG, "invalid n / nrhs for fit");
+  if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "fit workspace too small");
+  GPX_TRY(gpx_gram_f64(h, p, n, X, ldx, K, ldk));
+  GPX_TRY(gpx_potrf_f64(h, n, K, ldk, Dinv, info));
+  GPX_TRY(gpx_trtri_f64(h, n, K, ldk, Dinv, W, ldw, ws, ws_bytes));
+  return gpx_alpha_f64(h, n, W, ldw, Y, ldy, nrhs, p->const_mean, alpha, ws, ws_bytes);
+}
+
+gpx_status gpx_fit_f64_sync(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                            const double* Y, int64_t ldy, int64_t nrhs, double* K, int64_t ldk, double* Dinv,
+                            double* W, int64_t ldw, double* alpha, int32_t* info, void* ws, size_t ws_bytes,
+                            int32_t* info_host) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_TRY(gpx_fit_f64(h, p, n, X, ldx, Y, ldy, nrhs, K, ldk, Dinv, W, ldw, alpha, info, ws, ws_bytes));
+  int32_t hinfo = 0;
+  GPX_TRY(hip_check(c, hipMemcpyAsync(&hinfo, info, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream), "info D2H"));
+  GPX_TRY(hip_check(c, hipStreamSynchronize(c->stream), "sync"));
+  if (info_host) *info_host = hinfo;
+  if (hinfo != 0)
+    return fail(c, GPX_NOT_PD, "Gram matrix not positive definite at pivot " + std::to_string(hinfo - 1));
+  return GPX_OK;
+}
+
+gpx_status gpx_sweep_workspace_size(int64_t n, int64_t nrhs, int64_t m, size_t* bytes) {
+  if (!bytes || n < 1 || m < 1 || nrhs < 1 || nrhs > GPX_MAX_RHS) return GPX_INVALID_ARG;
+  *bytes = gpx::sweep_workspace_bytes(padded(n), nrhs, m);
+  return GPX_OK;
+}
+
+static gpx_status carve_sweep(Context* c, int64_t npad, int64_t nrhs, int64_t m, void* ws, size_t ws_bytes,
+                              gpx::SweepBuffers* b) {
+  if (!ws) return fail(c, GPX_INVALID_ARG, "sweep workspace is NULL");
+  if (ws_bytes < gpx::sweep_workspace_bytes(npad, nrhs, m)) return fail(c, GPX_INVALID_ARG, "sweep workspace too small");
+  const int64_t C = gpx::sweep_chunk_size(npad, m);
+  double* base = align256(ws);
+  b->chunk = C;
+  b->kstar = base;
+  b->mu_part = b->kstar + (size_t)npad * C;
+  b->ss_part = b->mu_part + (size_t)(npad / gpx::NB) * nrhs * C;
+  b->rec_val = b->ss_part + (size_t)(npad / 128) * C;
+  const int64_t nrec = (m + 255) / 256 + 1;
+  b->rec_idx = reinterpret_cast<int64_t*>(b->rec_val + nrec);
+  return GPX_OK;
+}
+
+gpx_status gpx_posterior_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                             const double* W, int64_t ldw, const double* alpha, int64_t nrhs, const double* Xs,
+                             int64_t m, int64_t ldxs, const double* y_mean_host, const double* y_scale_host,
+                             double* mean_out, int64_t ldmean, double* var_out, void* ws, size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_TRY(check_params(c, p));
+  GPX_TRY(check_n(c, n));
+  if (nrhs < 1 || nrhs > GPX_MAX_RHS) return fail(c, GPX_INVALID_ARG, "nrhs must be in [1, 8]");
+  if (m < 1) return fail(c, GPX_INVALID_ARG, "m must be >= 1");
+  GPX_NONNULL(c, X);
+  GPX_NONNULL(c, W);
+  GPX_NONNULL(c, alpha);
+  GPX_NONNULL(c, Xs);
+  GPX_NONNULL(c, mean_out);
+  GPX_NONNULL(c, var_out);
+  const int64_t npad = padded(n);
+  GPX_TRY(check_ld(c, ldx, p->d, "X", false));
+  GPX_TRY(check_ld(c, ldw, npad, "W", true));
+  GPX_TRY(check_ld(c, ldxs, p->d, "Xs", false));
+  GPX_TRY(check_ld(c, ldmean, nrhs, "mean", false));
+  gpx::SweepBuffers b;
+  GPX_TRY(carve_sweep(c, npad, nrhs, m, ws, ws_bytes, &b));
+  GPX_TRY(use_device(c));
+  for (int64_t s = 0; s < m; s += b.chunk) {
+    const int64_t mc = (m - s) < b.chunk ? (m - s) : b.chunk;
+    GPX_TRY(hip_check(c,
+                      gpx::launch_sweep_chunk(c, *p, (int)n, (int)npad, X, ldx, W, ldw, alpha, (int)nrhs, Xs + s * ldxs,
+                                              ldxs, mc, b, 0, nullptr, y_mean_host, y_scale_host,
+                                              mean_out + s * ldmean, ldmean, var_out + s, nullptr, 0, 0),
+                      "posterior"));
+  }
+  return GPX_OK;
+}
+
+gpx_status gpx_acquire_argmax_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                                  const double* W, int64_t ldw, const double* alpha, const double* Xs, int64_t m,
+                                  int64_t ldxs, const gpx_acq_params* a, int64_t index_offset, double* best_val,
+                                  int64_t* best_idx, double* scores_out, void* ws, size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_TRY(check_params(c, p));
+  GPX_TRY(check_n(c, n));
+  if (m < 1) return fail(c, GPX_INVALID_ARG, "m must be >= 1");
+  if (!a) return fail(c, GPX_INVALID_ARG, "acquisition params pointer is NULL");
+  if (a->kind < GPX_ACQ_EI || a->kind > GPX_ACQ_VARIANCE) return fail(c, GPX_INVALID_ARG, "unknown acquisition kind");
+  if (!(a->y_scale > 0.0)) return fail(c, GPX_INVALID_ARG, "y_scale must be positive");
+  if (a->kind == GPX_ACQ_UCB && !(a->beta >= 0.0)) return fail(c, GPX_INVALID_ARG, "UCB beta must be >= 0");
+  if (index_offset < 0) return fail(c, GPX_INVALID_ARG, "index_offset must be >= 0");
+  GPX_NONNULL(c, X);
+  GPX_NONNULL(c, W);
+  GPX_NONNULL(c, alpha);
+  GPX_NONNULL(c, Xs);
+  GPX_NONNULL(c, best_val);
+  GPX_NONNULL(c, best_idx);
+  const int64_t npad = padded(n);
+  GPX_TRY(check_ld(c, ldx, p->d, "X", false));
+  GPX_TRY(check_ld(c, ldw, npad, "W", true));
+  GPX_TRY(check_ld(c, ldxs, p->d, "Xs", false));
+  gpx::SweepBuffers b;
+  GPX_TRY(carve_sweep(c, npad, 1, m, ws, ws_bytes, &b));
+  GPX_TRY(use_device(c));
+  int64_t rec = 0;
+  for (int64_t s = 0; s < m; s += b.chunk) {
+    const int64_t mc = (m - s) < b.chunk ? (m - s) : b.chunk;
+    GPX_TRY(hip_check(c,
+                      gpx::launch_sweep_chunk(c, *p, (int)n, (int)npad, X, ldx, W, ldw, alpha, 1, Xs + s * ldxs, ldxs,
+                                              mc, b, 1, a, nullptr, nullptr, nullptr, 0, nullptr,
+                                              scores_out ? scores_out + s : nullptr, rec, index_offset + s),
+                      "acquire"));
+    rec += (mc + 255) / 256;
+  }
+  return hip_check(c, gpx::launch_argmax_final(c, b.rec_val, b.rec_idx, rec, best_val, best_idx), "argmax");
+}
+
+gpx_status gpx_argmax_combine_f64(gpx_handle h, const double* vals, const int64_t* idx, int64_t count,
+                                  double* best_val, int64_t* best_idx) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  if (count < 1) return fail(c, GPX_INVALID_ARG, "count must be >= 1");
+  GPX_NONNULL(c, vals);
+  GPX_NONNULL(c, idx);
+  GPX_NONNULL(c, best_val);
+  GPX_NONNULL(c, best_idx);
+  GPX_TRY(use_device(c));
+  return hip_check(c, gpx::launch_argmax_final(c, vals, idx, count, best_val, best_idx), "argmax_combine");
+}
+
+gpx_status gpx_timing_enable(gpx_handle h, int32_t mask) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  c->timing_mask = mask;
+  return GPX_OK;
+}
+
+gpx_status gpx_timing_reset(gpx_handle h) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  if (!c->pending.empty()) (void)hipStreamSynchronize(c->stream);
+  for (auto& pt : c->pending) {
+    c->free_events.push_back(pt.start);
+    c->free_events.push_back(pt.stop);
+  }
+  c->pending.clear();
+  for (int t = 0; t < GPX_TIMER_COUNT; ++t) {
+    c->timer_ms[t] = 0.0;
+    c->timer_launches[t] = 0;
+  }
+  return GPX_OK;
+}
+
+gpx_status gpx_timing_query(gpx_handle h, int32_t timer, double* total_ms_host, int64_t* launches_host) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  if (timer < 0 || timer >= GPX_TIMER_COUNT) return fail(c, GPX_INVALID_ARG, "unknown timer");
+  if (!c->pending.empty()) {
+    GPX_TRY(hip_check(c, hipStreamSynchronize(c->stream), "timing sync"));
+    for (auto& pt : c->pending) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, pt.start, pt.stop) == hipSuccess) {
+        c->timer_ms[pt.timer] += ms;
+        c->timer_launches[pt.timer] += 1;
+      }
+      c->free_events.push_back(pt.start);
+      c->free_events.push_back(pt.stop);
+    }
+    c->pending.clear();
+  }
+  if (total_ms_host) *total_ms_host = c->timer_ms[timer];
+  if (launches_host) *launches_host = c->timer_launches[timer];
+  return GPX_OK;
+}
+
+}  // extern "C"

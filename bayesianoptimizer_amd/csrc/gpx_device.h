@@ -1,0 +1,183 @@
+// Device-side helpers shared by the gpx kernels: covariance evaluation, triangular tile decoding and the
+// fp64 MFMA tile core (v_mfma_f64_16x16x4_f64, 64-lane waves).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "gpx_internal.h"
+
+namespace gpx {
+
+// ---- covariance ---------------------------------------------------------------------------------
+// Matches oracle/gp_oracle.py::kernel_matrix term for term: r2 is the sum over dimensions of
+// ((a_k - b_k) / l_k)^2 accumulated in order k = 0..d-1, `lin` the ARD linear term.
+__device__ __forceinline__ double cov_from_r2(int kind, double outputscale, double r2, double lin) {
+  if (kind == GPX_KERNEL_RBF) return outputscale * exp(-0.5 * r2);
+  const double r = sqrt(r2);
+  const double s5r = 2.23606797749978969640917366873128 * r;  // sqrt(5) r
+  const double m = (1.0 + s5r + (5.0 / 3.0) * r2) * exp(-s5r);
+  if (kind == GPX_KERNEL_MATERN52) return outputscale * m;
+  return outputscale * (lin + m);
+}
+
+// Linear index t over the lower triangle of an m x m block grid (row-major order of (i, j), j <= i)
+// -> (i, j).
+__device__ __forceinline__ void tri_decode(int t, int& i, int& j) {
+  int r = (int)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+  while ((r + 1) * (r + 2) / 2 <= t) ++r;
+  while (r * (r + 1) / 2 > t) --r;
+  i = r;
+  j = t - r * (r + 1) / 2;
+}
+
+__device__ __forceinline__ d4 mfma16x16x4(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// ---- fp64 MFMA GEMM tile core ---------------------------------------------------------------------
+// One 256-thread workgroup computes a TM x TN tile C = sum_k A(m,k) B(k,n) over k in [kbeg, kend)
+// (multiples of BK).  Four waves in a 2x2 arrangement each own a (TM/2) x (TN/2) sub-tile made of
+// (TM/32) x (TN/32) MFMA 16x16 blocks.
+//   A_KMAJOR: A(m,k) at A[k*lda + m]  else A[m*lda + k]
+//   B_KMAJOR: B(k,n) at B[k*ldb + n]  else B[n*ldb + k]
+// Operands are staged global -> registers -> LDS (k-major, rows padded by 16 doubles so the two
+// 16-lane halves of each ds_read_b64 group hit disjoint banks), double-buffered with one barrier per
+// k-tile; the next k-tile's global loads are issued before the current tile's MFMAs.
+// Accumulator layout (measured on gfx950, tools/probes/mfma_f64_probe.hip):
+//   acc[i][j][r] holds C(row = wm0 + 16 i + (lane>>4) + 4 r, col = wn0 + 16 j + (lane&15)).
+template <int TM, int TN, int BK, bool A_KMAJOR, bool B_KMAJOR>
+struct MfmaTile {
+  static constexpr int WM = TM / 32;  // MFMA blocks per wave along m
+  static constexpr int WN = TN / 32;
+  static constexpr int PA = TM + 16;  // padded LDS row lengths
+  static constexpr int PB = TN + 16;
+  static constexpr int LDS_DOUBLES = 2 * BK * (PA + PB);
+  // register staging: each thread moves 2 consecutive doubles per load
+  static constexpr int A_LOADS = TM * BK / (2 * WG);
+  static constexpr int B_LOADS = TN * BK / (2 * WG);
+  static_assert(A_LOADS >= 1 && B_LOADS >= 1, "tile too small for 256 threads");
+
+  d4 acc[WM][WN];
+  double2 ra[A_LOADS], rb[B_LOADS];
+
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+  }
+
+  // global -> registers for the k-tile starting at k0
+  __device__ __forceinline__ void load_regs(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
+                                            int64_t ldb, int k0) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < A_LOADS; ++q) {
+      int e = (t + q * WG) * 2;  // element offset inside the BK x TM (k-major) or TM x BK tile
+      if (A_KMAJOR) {
+        int kk = e / TM, mm = e % TM;
+        ra[q] = *reinterpret_cast<const double2*>(A + (int64_t)(k0 + kk) * lda + mm);
+      } else {
+        int mm = e / BK, kk = e % BK;
+        ra[q] = *reinterpret_cast<const double2*>(A + (int64_t)mm * lda + k0 + kk);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < B_LOADS; ++q) {
+      int e = (t + q * WG) * 2;
+      if (B_KMAJOR) {
+        int kk = e / TN, nn = e % TN;
+        rb[q] = *reinterpret_cast<const double2*>(B + (int64_t)(k0 + kk) * ldb + nn);
+      } else {
+        int nn = e / BK, kk = e % BK;
+        rb[q] = *reinterpret_cast<const double2*>(B + (int64_t)nn * ldb + k0 + kk);
+      }
+    }
+  }
+
+  // registers -> LDS buffer
+  __device__ __forceinline__ void store_lds(double* sA, double* sB) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < A_LOADS; ++q) {
+      int e = (t + q * WG) * 2;
+      if (A_KMAJOR) {
+        int kk = e / TM, mm = e % TM;
+        *reinterpret_cast<double2*>(sA + kk * PA + mm) = ra[q];
+      } else {
+        int mm = e / BK, kk = e % BK;
+        sA[kk * PA + mm] = ra[q].x;
+        sA[(kk + 1) * PA + mm] = ra[q].y;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < B_LOADS; ++q) {
+      int e = (t + q * WG) * 2;
+      if (B_KMAJOR) {
+        int kk = e / TN, nn = e % TN;
+        *reinterpret_cast<double2*>(sB + kk * PB + nn) = rb[q];
+      } else {
+        int nn = e / BK, kk = e % BK;
+        sB[kk * PB + nn] = rb[q].x;
+        sB[(kk + 1) * PB + nn] = rb[q].y;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void compute(const double* sA, const double* sB) {
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int wm0 = (w >> 1) * (TM / 2);
+    const int wn0 = (w & 1) * (TN / 2);
+    const int kr = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int ks = 0; ks < BK; ks += 4) {
+      double a[WM], b[WN];
+#pragma unroll
+      for (int i = 0; i < WM; ++i) a[i] = sA[(ks + kr) * PA + wm0 + 16 * i + cl];
+#pragma unroll
+      for (int j = 0; j < WN; ++j) b[j] = sB[(ks + kr) * PB + wn0 + 16 * j + cl];
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j) acc[i][j] = mfma16x16x4(a[i], b[j], acc[i][j]);
+    }
+  }
+
+  // Full k loop. smem must hold LDS_DOUBLES doubles.  A/B point at the tile origin (m0 / n0 applied).
+  __device__ __forceinline__ void run(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
+                                      int64_t ldb, int kbeg, int kend, double* smem) {
+    zero();
+    if (kend <= kbeg) return;
+    double* sA0 = smem;
+    double* sB0 = smem + BK * PA;
+    double* sA1 = smem + BK * (PA + PB);
+    double* sB1 = sA1 + BK * PA;
+    load_regs(A, lda, B, ldb, kbeg);
+    store_lds(sA0, sB0);
+    __syncthreads();
+    int it = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += BK, ++it) {
+      const bool more = (k0 + BK) < kend;
+      if (more) load_regs(A, lda, B, ldb, k0 + BK);
+      if ((it & 1) == 0) {
+        compute(sA0, sB0);
+        if (more) store_lds(sA1, sB1);
+      } else {
+        compute(sA1, sB1);
+        if (more) store_lds(sA0, sB0);
+      }
+      __syncthreads();
+    }
+  }
+
+  // Row / column of accumulator element (i, j, r) for this lane, relative to the tile origin.
+  __device__ __forceinline__ static int row_of(int i, int r) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    return (w >> 1) * (TM / 2) + 16 * i + (lane >> 4) + 4 * r;
+  }
+  __device__ __forceinline__ static int col_of(int j) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    return (w & 1) * (TN / 2) + 16 * j + (lane & 15);
+  }
+};
+
+}  // namespace gpx

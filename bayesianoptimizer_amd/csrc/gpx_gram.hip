@@ -1,0 +1,84 @@
+// Gram builder: K(X,X) + (noise + jitter) I, lower 64x64 tiles of the padded matrix.
+// SURVEY §8a row a3 — replaces the covar_module(X) evaluation inside GPyTorch's ExactGP path [upstream]
+// (optimization/Bayesian.py:91-93, optimization/Bayesian6.py:471-484).
+//
+// HBM-write-bound: each 64x64 tile is written once (32 KiB); inputs are two 64 x d slices of X staged in
+// LDS (lengthscale-divided copy for the stationary part, raw copy for the linear part).  Each wave owns
+// one row of the tile at a time and writes 64 consecutive doubles (512 B) per store instruction.
+#include "gpx_internal.h"
+#include "gpx_device.h"
+
+namespace gpx {
+
+template <int DMAX>
+__global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, int nblk, const double* __restrict__ X,
+                                                  int64_t ldx, double* __restrict__ K, int64_t ldk) {
+  __shared__ double si[NB][DMAX + 1], sj[NB][DMAX + 1];    // scaled x / l
+  __shared__ double ri[NB][DMAX + 1], rj[NB][DMAX + 1];    // raw x (linear kernel)
+  int ti, tj;
+  tri_decode(blockIdx.x, ti, tj);
+  const int i0 = ti * NB, j0 = tj * NB;
+  const int d = p.d;
+  const bool lin = (p.kind == GPX_KERNEL_SCALE_LINEAR_MATERN52);
+  for (int e = threadIdx.x; e < NB * DMAX; e += WG) {
+    int r = e / DMAX, k = e % DMAX;
+    double xi = 0.0, xj = 0.0;
+    if (k < d) {
+      if (i0 + r < n) xi = X[(int64_t)(i0 + r) * ldx + k];
+      if (j0 + r < n) xj = X[(int64_t)(j0 + r) * ldx + k];
+    }
+    const double l = (k < d) ? p.lengthscale[k] : 1.0;
+    si[r][k] = xi / l;
+    sj[r][k] = xj / l;
+    ri[r][k] = xi * ((k < d) ? p.linear_variance[k] : 0.0);
+    rj[r][k] = xj;
+  }
+  __syncthreads();
+  const int c = threadIdx.x & 63;
+  const int gj = j0 + c;
+  double xc[DMAX], rc[DMAX];
+#pragma unroll
+  for (int k = 0; k < DMAX; ++k) {
+    xc[k] = sj[c][k];
+    rc[k] = rj[c][k];
+  }
+  const double diag_add = p.noise + p.jitter;
+  for (int r = threadIdx.x >> 6; r < NB; r += 4) {
+    const int gi = i0 + r;
+    double v;
+    if (gi < n && gj < n) {
+      double r2 = 0.0, lv = 0.0;
+#pragma unroll
+      for (int k = 0; k < DMAX; ++k) {
+        if (k < d) {
+          const double df = si[r][k] - xc[k];
+          r2 += df * df;
+          if (lin) lv += ri[r][k] * rc[k];
+        }
+      }
+      v = cov_from_r2(p.kind, p.outputscale, r2, lv);
+      if (gi == gj) v += diag_add;
+    } else {
+      v = (gi == gj) ? 1.0 : 0.0;  // identity padding
+    }
+    K[(int64_t)gi * ldk + gj] = v;
+  }
+}
+
+hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
+                       double* K, int64_t ldk) {
+  LaunchTimer tm(c, GPX_TIMER_GRAM);
+  const int nblk = npad / NB;
+  const int tiles = nblk * (nblk + 1) / 2;
+  if (p.d <= 4)
+    gram_kernel<4><<<tiles, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk);
+  else if (p.d <= 8)
+    gram_kernel<8><<<tiles, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk);
+  else if (p.d <= 16)
+    gram_kernel<16><<<tiles, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk);
+  else
+    gram_kernel<32><<<tiles, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk);
+  return hipGetLastError();
+}
+
+}  // namespace gpx

@@ -1,0 +1,75 @@
+// Internal declarations shared by the gpx HIP translation units (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstddef>
+#include <string>
+#include <vector>
+#include "../../include/gpx.h"
+
+namespace gpx {
+
+constexpr int NB = 64;              // Cholesky / TRTRI block (64x64 diagonal blocks)
+constexpr int TILE = GPX_TILE;      // padding granule and sweep tile (128)
+constexpr int WG = 256;             // threads per workgroup (4 waves of 64)
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// ---- context -----------------------------------------------------------------------------------
+struct PendingTimer {
+  int timer;
+  hipEvent_t start, stop;
+};
+
+struct Context {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string last_error;
+  int32_t timing_mask = 0;
+  double timer_ms[GPX_TIMER_COUNT] = {0};
+  int64_t timer_launches[GPX_TIMER_COUNT] = {0};
+  std::vector<PendingTimer> pending;
+  std::vector<hipEvent_t> free_events;
+};
+
+// Scoped timer: records a start event on construction and a stop event on destruction when the
+// timer's bit is set in the context's mask.
+struct LaunchTimer {
+  Context* c;
+  int timer;
+  hipEvent_t s = nullptr, e = nullptr;
+  LaunchTimer(Context* ctx, int t);
+  ~LaunchTimer();
+};
+
+// ---- launch wrappers (defined in the .hip files) -------------------------------------------------
+hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
+                       double* K, int64_t ldk);
+hipError_t launch_potrf(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info);
+hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, const double* Dinv, double* W,
+                        int64_t ldw, double* T);
+hipError_t launch_alpha(Context* c, int n, int npad, const double* W, int64_t ldw, const double* Y, int64_t ldy,
+                        int nrhs, double const_mean, double* alpha, double* zpart, double* z);
+
+struct SweepBuffers {
+  double* kstar;     // npad x C
+  double* mu_part;   // (npad/64) x nrhs x C
+  double* ss_part;   // (npad/128) x C
+  double* rec_val;   // records (one per 256-candidate block over the whole sweep)
+  int64_t* rec_idx;
+  int64_t chunk;     // C
+};
+// mode 0: posterior (write mean/var); mode 1: acquisition (records + optional scores)
+hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
+                              const double* W, int64_t ldw, const double* alpha, int nrhs, const double* Xs,
+                              int64_t ldxs, int64_t m_chunk, const SweepBuffers& b, int mode,
+                              const gpx_acq_params* a, const double* y_mean, const double* y_scale,
+                              double* mean_out, int64_t ldmean, double* var_out, double* scores_out,
+                              int64_t rec_offset, int64_t index_offset);
+hipError_t launch_argmax_final(Context* c, const double* vals, const int64_t* idx, int64_t count, double* best_val,
+                               int64_t* best_idx);
+
+int64_t sweep_chunk_size(int64_t npad, int64_t m);
+size_t sweep_workspace_bytes(int64_t npad, int64_t nrhs, int64_t m);
+
+}  // namespace gpx

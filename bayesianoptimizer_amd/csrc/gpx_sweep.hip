@@ -1,0 +1,359 @@
+// Posterior / acquisition sweep over a chunk of C candidates.
+// Replaces model.posterior(X) (optimization/Bayesian2.py:169-171, optimization/Bayesian6.py:615-617,688-690),
+// the raw-sample sweep + argmax inside optimize_acqf (optimization/Bayesian.py:105-113) and the pool scan +
+// top-k of optimization/Bayesian7.py:646-681.
+//
+// Per chunk, three launches:
+//  1. kstar_kernel   K*[j][c] = k(x_j, xs_c) for all padded rows j (row-major npad x C, zero for j >= n),
+//                    and the partial means mu_part[jb][r][c] = sum_{j in block jb} alpha[j][r] K*[j][c].
+//  2. trmm_sumsq     V = L^{-1} K* = W^T K* as a triangular fp64-MFMA product (128x128 tiles, k < (I+1)*128
+//                    for row tile I), never stored: each workgroup writes the column sums of V^2 over its 128
+//                    rows into ss_part[I][c].  This is the n^2-flops-per-candidate term and the dominant
+//                    kernel of the whole hot path.
+//  3. finalize       mu = m + sum mu_part, var = k** - sum ss_part (fixed summation order: deterministic),
+//                    GPyTorch/BoTorch variance floors, Standardize untransform, analytic acquisition, and a
+//                    256-candidate block argmax record (max value, then lowest index; NaN never wins).
+// launch_argmax_final reduces the records of the whole sweep in one workgroup.
+#include "gpx_internal.h"
+#include "gpx_device.h"
+
+namespace gpx {
+
+// ---- acquisition math (BoTorch analytic forms [upstream], restated; oracle/gp_oracle.py mirrors them) ----
+__device__ __forceinline__ double ndtr_d(double a) {  // standard normal cdf, cephes-style branches
+  const double x = a * 0.70710678118654752440084436210485;
+  const double z = fabs(x);
+  if (z < 0.70710678118654752440084436210485) return 0.5 + 0.5 * erf(x);
+  const double y = 0.5 * erfc(z);
+  return (x > 0.0) ? 1.0 - y : y;
+}
+__device__ __forceinline__ double phi_d(double u) { return exp(-0.5 * u * u) * 0.39894228040143267793994605993438; }
+__device__ __forceinline__ double ei_helper_d(double u) { return phi_d(u) + u * ndtr_d(u); }
+__device__ __forceinline__ double log1mexp_d(double x) {
+  return (x > -0.69314718055994530941723212145818) ? log(-expm1(x)) : log1p(-exp(x));
+}
+__device__ __forceinline__ double log_ei_helper_d(double u) {
+  const double neg_inv_sqrt_eps = -67108864.0;  // -1/sqrt(2^-52)
+  if (u > -1.0) return log(ei_helper_d(u));
+  const double u_eps = fmax(u, neg_inv_sqrt_eps);
+  const double w = log(erfcx(-u_eps * 0.70710678118654752440084436210485) * fabs(u_eps)) +
+                   0.22579135264472743236309761494744;  // log(sqrt(pi/2))
+  const double log_phi = -0.5 * u * u - 0.91893853320467274178032973640562;  // log(sqrt(2 pi))
+  if (u > neg_inv_sqrt_eps) return log_phi + log1mexp_d(w);
+  return log_phi - 2.0 * log(fabs(u));
+}
+__device__ __forceinline__ double acq_score(int kind, double mu, double var, double best_f, double beta) {
+  const double sigma = sqrt(var);
+  if (kind == GPX_ACQ_EI) return sigma * ei_helper_d((mu - best_f) / sigma);
+  if (kind == GPX_ACQ_LOGEI) return log_ei_helper_d((mu - best_f) / sigma) + log(sigma);
+  if (kind == GPX_ACQ_UCB) return mu + sqrt(beta) * sigma;
+  return var;
+}
+
+// (value, index) order: larger value wins, equal values -> lower index; NaN already mapped to -inf.
+__device__ __forceinline__ void argmax_merge(double& v, int64_t& i, double v2, int64_t i2) {
+  if (v2 > v || (v2 == v && i2 < i)) {
+    v = v2;
+    i = i2;
+  }
+}
+
+template <int DMAX>
+__device__ __forceinline__ void load_point(const gpx_kernel_params& p, const double* __restrict__ x, bool valid,
+                                           double (&xs)[DMAX], double (&xr)[DMAX]) {
+#pragma unroll
+  for (int k = 0; k < DMAX; ++k) {
+    const double v = (valid && k < p.d) ? x[k] : 0.0;
+    xs[k] = (k < p.d) ? v / p.lengthscale[k] : 0.0;
+    xr[k] = v;
+  }
+}
+
+// ---- 1. K* and partial means ---------------------------------------------------------------------------
+template <int DMAX>
+__global__ void __launch_bounds__(WG) kstar_kernel(gpx_kernel_params p, int n, const double* __restrict__ X,
+                                                   int64_t ldx, const double* __restrict__ alpha, int nrhs,
+                                                   const double* __restrict__ Xs, int64_t ldxs, int64_t m_chunk,
+                                                   int64_t C, double* __restrict__ kstar,
+                                                   double* __restrict__ mu_part) {
+  __shared__ double sx[NB][DMAX + 1], sr[NB][DMAX + 1], sa[NB][GPX_MAX_RHS];
+  const int jb = blockIdx.y;
+  const int j0 = jb * NB;
+  const int d = p.d;
+  const bool lin = (p.kind == GPX_KERNEL_SCALE_LINEAR_MATERN52);
+  for (int e = threadIdx.x; e < NB * DMAX; e += WG) {
+    const int r = e / DMAX, k = e % DMAX;
+    double v = 0.0;
+    if (k < d && j0 + r < n) v = X[(int64_t)(j0 + r) * ldx + k];
+    sx[r][k] = (k < d) ? v / p.lengthscale[k] : 0.0;
+    sr[r][k] = (k < d) ? v * p.linear_variance[k] : 0.0;
+  }
+  for (int e = threadIdx.x; e < NB * nrhs; e += WG) {
+    const int r = e / nrhs, q = e % nrhs;
+    sa[r][q] = alpha[(int64_t)(j0 + r) * nrhs + q];
+  }
+  __syncthreads();
+  const int64_t c = (int64_t)blockIdx.x * WG + threadIdx.x;
+  const bool valid = c < m_chunk;
+  double xs[DMAX], xr[DMAX];
+  load_point<DMAX>(p, Xs + (valid ? c * ldxs : 0), valid, xs, xr);
+  double mu[GPX_MAX_RHS];
+#pragma unroll
+  for (int q = 0; q < GPX_MAX_RHS; ++q) mu[q] = 0.0;
+  for (int j = 0; j < NB; ++j) {
+    double kv = 0.0;
+    if (j0 + j < n) {
+      double r2 = 0.0, lv = 0.0;
+#pragma unroll
+      for (int k = 0; k < DMAX; ++k) {
+        if (k < d) {
+          const double df = sx[j][k] - xs[k];
+          r2 += df * df;
+          if (lin) lv += sr[j][k] * xr[k];
+        }
+      }
+      kv = cov_from_r2(p.kind, p.outputscale, r2, lv);
+    }
+    kstar[(int64_t)(j0 + j) * C + c] = kv;
+#pragma unroll
+    for (int q = 0; q < GPX_MAX_RHS; ++q)
+      if (q < nrhs) mu[q] += sa[j][q] * kv;
+  }
+  for (int q = 0; q < nrhs; ++q) mu_part[((int64_t)jb * nrhs + q) * C + c] = mu[q];
+}
+
+// ---- 2. triangular product + column sums of squares ------------------------------------------------------
+constexpr int TT = 128;  // trmm tile (rows of V x candidates)
+using TrmmTile = MfmaTile<TT, TT, 16, true, true>;
+
+__global__ void __launch_bounds__(WG) trmm_sumsq_kernel(const double* __restrict__ W, int64_t ldw,
+                                                        const double* __restrict__ kstar, int64_t C, int nI,
+                                                        double* __restrict__ ss_part) {
+  __shared__ __attribute__((aligned(16))) double smem[TrmmTile::LDS_DOUBLES];
+  const int I = nI - 1 - blockIdx.y;  // heaviest row tiles are dispatched first
+  const int cb = blockIdx.x;
+  const double* Ab = W + (int64_t)I * TT;            // A(m=i,k) = W[k][I*128 + i]
+  const double* Bb = kstar + (int64_t)cb * TT;       // B(k,n=c) = K*[k][cb*128 + c]
+  TrmmTile tile;
+  tile.run(Ab, ldw, Bb, C, 0, (I + 1) * TT, smem);
+  // column sums of squares over this wave's rows, then over the lanes holding the same column
+  double s[TrmmTile::WN];
+#pragma unroll
+  for (int j = 0; j < TrmmTile::WN; ++j) {
+    double v = 0.0;
+#pragma unroll
+    for (int i = 0; i < TrmmTile::WM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v += tile.acc[i][j][r] * tile.acc[i][j][r];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    s[j] = v;
+  }
+  // the two waves of each column half (w>>1 = 0, 1) combine through LDS (smem is free after run())
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double* red = smem;
+  if ((w >> 1) == 1 && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < TrmmTile::WN; ++j) red[TrmmTile::col_of(j)] = s[j];
+  }
+  __syncthreads();
+  if ((w >> 1) == 0 && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < TrmmTile::WN; ++j) {
+      const int col = TrmmTile::col_of(j);
+      ss_part[(int64_t)I * C + (int64_t)cb * TT + col] = s[j] + red[col];
+    }
+  }
+}
+
+// ---- 3. finalize: posterior (mode 0) or acquisition + block argmax (mode 1) ------------------------------
+struct FinalizeArgs {
+  gpx_kernel_params p;
+  double y_mean[GPX_MAX_RHS];
+  double y_scale[GPX_MAX_RHS];
+  int acq_kind;
+  double best_f, beta;
+};
+
+__global__ void __launch_bounds__(WG) finalize_kernel(FinalizeArgs fa, int mode, const double* __restrict__ Xs,
+                                                      int64_t ldxs, int64_t m_chunk, int64_t C, int nrhs, int nJB,
+                                                      int nI, const double* __restrict__ mu_part,
+                                                      const double* __restrict__ ss_part,
+                                                      double* __restrict__ mean_out, int64_t ldmean,
+                                                      double* __restrict__ var_out, double* __restrict__ scores_out,
+                                                      double* __restrict__ rec_val, int64_t* __restrict__ rec_idx,
+                                                      int64_t index_base) {
+  const gpx_kernel_params& p = fa.p;
+  const int64_t c = (int64_t)blockIdx.x * WG + threadIdx.x;
+  const bool valid = c < m_chunk;
+  double score = -INFINITY;
+  if (valid) {
+    // prior variance k(x, x)
+    double kd = p.outputscale;
+    if (p.kind == GPX_KERNEL_SCALE_LINEAR_MATERN52) {
+      double lv = 0.0;
+      for (int k = 0; k < p.d; ++k) {
+        const double v = Xs[c * ldxs + k];
+        lv += v * v * p.linear_variance[k];
+      }
+      kd = p.outputscale * (lv + 1.0);
+    }
+    double ss = 0.0;
+    for (int I = 0; I < nI; ++I) ss += ss_part[(int64_t)I * C + c];
+    double var = fmax(kd - ss, 1e-10);  // gpytorch min_variance (float64) [upstream]
+    if (mode == 0) {
+      for (int q = 0; q < nrhs; ++q) {
+        double mu = 0.0;
+        for (int jb = 0; jb < nJB; ++jb) mu += mu_part[((int64_t)jb * nrhs + q) * C + c];
+        mu += p.const_mean;
+        mean_out[c * ldmean + q] = fa.y_mean[q] + fa.y_scale[q] * mu;
+      }
+      var_out[c] = fmax(var * (fa.y_scale[0] * fa.y_scale[0]), 1e-12);  // BoTorch min_var [upstream]
+      return;
+    }
+    double mu = 0.0;
+    for (int jb = 0; jb < nJB; ++jb) mu += mu_part[(int64_t)jb * C + c];
+    mu = fa.y_mean[0] + fa.y_scale[0] * (mu + p.const_mean);
+    var = fmax(var * (fa.y_scale[0] * fa.y_scale[0]), 1e-12);
+    score = acq_score(fa.acq_kind, mu, var, fa.best_f, fa.beta);
+    if (scores_out) scores_out[c] = score;
+    if (score != score) score = -INFINITY;
+  }
+  if (mode == 0) return;
+  // block argmax
+  double bv = score;
+  int64_t bi = valid ? index_base + c : INT64_MAX;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double v2 = __shfl_xor(bv, o);
+    const int64_t i2 = __shfl_xor(bi, o);
+    argmax_merge(bv, bi, v2, i2);
+  }
+  __shared__ double wv[4];
+  __shared__ int64_t wi[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    wv[w] = bv;
+    wi[w] = bi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < 4; ++q) argmax_merge(bv, bi, wv[q], wi[q]);
+    rec_val[blockIdx.x] = bv;
+    rec_idx[blockIdx.x] = bi;
+  }
+}
+
+__global__ void __launch_bounds__(WG) argmax_final_kernel(const double* __restrict__ vals,
+                                                          const int64_t* __restrict__ idx, int64_t count,
+                                                          double* __restrict__ best_val,
+                                                          int64_t* __restrict__ best_idx) {
+  double bv = -INFINITY;
+  int64_t bi = INT64_MAX;
+  for (int64_t e = threadIdx.x; e < count; e += WG) {
+    double v = vals[e];
+    if (v != v) v = -INFINITY;
+    argmax_merge(bv, bi, v, idx[e]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double v2 = __shfl_xor(bv, o);
+    const int64_t i2 = __shfl_xor(bi, o);
+    argmax_merge(bv, bi, v2, i2);
+  }
+  __shared__ double wv[4];
+  __shared__ int64_t wi[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    wv[w] = bv;
+    wi[w] = bi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < 4; ++q) argmax_merge(bv, bi, wv[q], wi[q]);
+    *best_val = bv;
+    *best_idx = bi;
+  }
+}
+
+// ---- host side -------------------------------------------------------------------------------------------
+int64_t sweep_chunk_size(int64_t npad, int64_t m) {
+  // K* chunk capped at ~256 MiB (it is re-read (I+1) times by trmm_sumsq; keeping it near the 256 MiB
+  // Infinity Cache helps), at most 16384 candidates, multiple of 256.
+  int64_t cap = ((int64_t)1 << 25) / npad;  // doubles per row budget: 2^28 bytes / 8 / npad
+  cap = (cap / 256) * 256;
+  if (cap < 256) cap = 256;
+  if (cap > 16384) cap = 16384;
+  int64_t need = ((m + 255) / 256) * 256;
+  if (need < 256) need = 256;
+  return need < cap ? need : cap;
+}
+
+size_t sweep_workspace_bytes(int64_t npad, int64_t nrhs, int64_t m) {
+  const int64_t C = sweep_chunk_size(npad, m);
+  const int64_t nrec = (m + 255) / 256 + 1;
+  size_t b = 0;
+  b += (size_t)npad * C * 8;                 // kstar
+  b += (size_t)(npad / NB) * nrhs * C * 8;   // mu_part
+  b += (size_t)(npad / TT) * C * 8;          // ss_part
+  b += (size_t)nrec * 16;                    // records
+  return b + 256;
+}
+
+hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
+                              const double* W, int64_t ldw, const double* alpha, int nrhs, const double* Xs,
+                              int64_t ldxs, int64_t m_chunk, const SweepBuffers& b, int mode,
+                              const gpx_acq_params* a, const double* y_mean, const double* y_scale,
+                              double* mean_out, int64_t ldmean, double* var_out, double* scores_out,
+                              int64_t rec_offset, int64_t index_offset) {
+  const int64_t C = b.chunk;
+  const int nJB = npad / NB, nI = npad / TT;
+  const int ncb = (int)((m_chunk + WG - 1) / WG);  // 256-candidate blocks actually used in this chunk
+  {
+    LaunchTimer tm(c, GPX_TIMER_KSTAR);
+    dim3 g(ncb, nJB);
+    if (p.d <= 4)
+      kstar_kernel<4><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk, C, b.kstar, b.mu_part);
+    else if (p.d <= 8)
+      kstar_kernel<8><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk, C, b.kstar, b.mu_part);
+    else if (p.d <= 16)
+      kstar_kernel<16><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk, C, b.kstar, b.mu_part);
+    else
+      kstar_kernel<32><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk, C, b.kstar, b.mu_part);
+  }
+  {
+    LaunchTimer tm(c, GPX_TIMER_TRMM);
+    dim3 g((int)((m_chunk + TT - 1) / TT), nI);
+    trmm_sumsq_kernel<<<g, WG, 0, c->stream>>>(W, ldw, b.kstar, C, nI, b.ss_part);
+  }
+  {
+    LaunchTimer tm(c, GPX_TIMER_ACQ);
+    FinalizeArgs fa;
+    fa.p = p;
+    for (int q = 0; q < GPX_MAX_RHS; ++q) {
+      fa.y_mean[q] = (y_mean && q < nrhs) ? y_mean[q] : 0.0;
+      fa.y_scale[q] = (y_scale && q < nrhs) ? y_scale[q] : 1.0;
+    }
+    fa.acq_kind = a ? a->kind : 0;
+    fa.best_f = a ? a->best_f : 0.0;
+    fa.beta = a ? a->beta : 0.0;
+    if (a) {
+      fa.y_mean[0] = a->y_mean;
+      fa.y_scale[0] = a->y_scale;
+    }
+    finalize_kernel<<<ncb, WG, 0, c->stream>>>(fa, mode, Xs, ldxs, m_chunk, C, nrhs, nJB, nI, b.mu_part,
+                                                   b.ss_part, mean_out, ldmean, var_out, scores_out,
+                                                   b.rec_val + rec_offset, b.rec_idx + rec_offset,
+                                                   index_offset);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_argmax_final(Context* c, const double* vals, const int64_t* idx, int64_t count, double* best_val,
+                               int64_t* best_idx) {
+  LaunchTimer tm(c, GPX_TIMER_ACQ);
+  argmax_final_kernel<<<1, WG, 0, c->stream>>>(vals, idx, count, best_val, best_idx);
+  return hipGetLastError();
+}
+
+}  // namespace gpx

@@ -1,0 +1,179 @@
+// Triangular inverse W = L^{-T} (upper, row-major) and alpha = K^{-1}(y - m) = W W^T (y - m).
+// alpha is GPyTorch's mean_cache [upstream]; W turns every later solve L^{-1} k* of
+// the posterior/acquisition sweep into an independent triangular product (gpx_sweep.hip).
+//
+// TRTRI by recursive doubling over the 64x64 diagonal inverses D_k produced by potrf:
+//   level 0: W_kk = D_k^T, and the 64x64 block below the diagonal inside every 128-tile is zeroed;
+//   level l: for groups of 2h blocks (h = 2^(l-1)), with first half (off1, b1) and second half (off2, b2):
+//       T   = L21^T W22          (b1 x b2; W22 upper: k <= c)
+//       W12 = -W11 T             (b1 x b2; W11 upper: k >= r)
+//   two MFMA launches per level, all groups of a level batched in blockIdx.z: 1 + 2*ceil(log2(nblk))
+//   launches in total.  Works for any even number of 64-blocks (the last group may be partial).
+#include "gpx_internal.h"
+#include "gpx_device.h"
+
+namespace gpx {
+
+__global__ void __launch_bounds__(WG) trtri_diag_kernel(const double* __restrict__ Dinv, double* __restrict__ W,
+                                                        int64_t ldw) {
+  const int b = blockIdx.x;
+  const double* D = Dinv + (int64_t)b * NB * NB;
+  double* Wbb = W + (int64_t)b * NB * ldw + (int64_t)b * NB;
+  for (int e = threadIdx.x; e < NB * NB; e += WG) {
+    const int r = e / NB, c = e % NB;
+    Wbb[(int64_t)r * ldw + c] = D[c * NB + r];  // transpose: W_bb = D_b^T
+  }
+  if (b & 1) {  // zero the strictly-lower 64x64 block of this 128-tile
+    double* Z = W + (int64_t)b * NB * ldw + (int64_t)(b - 1) * NB;
+    for (int e = threadIdx.x; e < NB * NB; e += WG) Z[(int64_t)(e / NB) * ldw + (e % NB)] = 0.0;
+  }
+}
+
+// T_p = L21^T W22 for group p of level with half-size h blocks.
+__global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ L, int64_t ldl,
+                                                     const double* __restrict__ W, int64_t ldw,
+                                                     double* __restrict__ T, int h, int nblk) {
+  using Tile = MfmaTile<NB, NB, 16, true, true>;
+  __shared__ __attribute__((aligned(16))) double smem[Tile::LDS_DOUBLES];
+  const int p = blockIdx.z;
+  const int s1 = p * 2 * h, s2 = s1 + h;
+  const int nb2 = min(2 * h, nblk - s1) - h;
+  const int rb = blockIdx.y, cb = blockIdx.x;
+  if (nb2 <= 0 || cb >= nb2) return;
+  const int b1 = h * NB;
+  const int64_t off1 = (int64_t)s1 * NB, off2 = (int64_t)s2 * NB;
+  const double* Ab = L + off2 * ldl + off1 + rb * NB;   // A(m=r,k=q) = L[off2+q][off1+r]
+  const double* Bb = W + off2 * ldw + off2 + cb * NB;   // B(k=q,n=c) = W[off2+q][off2+c]
+  Tile tile;
+  tile.run(Ab, ldl, Bb, ldw, 0, (cb + 1) * NB, smem);
+  double* Tp = T + (int64_t)p * b1 * b1;
+#pragma unroll
+  for (int i = 0; i < Tile::WM; ++i)
+#pragma unroll
+    for (int j = 0; j < Tile::WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Tp[(int64_t)(rb * NB + Tile::row_of(i, r)) * b1 + cb * NB + Tile::col_of(j)] = tile.acc[i][j][r];
+}
+
+// W12 = -W11 T_p
+__global__ void __launch_bounds__(WG) trtri_w_kernel(double* __restrict__ W, int64_t ldw, const double* __restrict__ T,
+                                                     int h, int nblk) {
+  using Tile = MfmaTile<NB, NB, 16, false, true>;
+  __shared__ __attribute__((aligned(16))) double smem[Tile::LDS_DOUBLES];
+  const int p = blockIdx.z;
+  const int s1 = p * 2 * h, s2 = s1 + h;
+  const int nb2 = min(2 * h, nblk - s1) - h;
+  const int rb = blockIdx.y, cb = blockIdx.x;
+  if (nb2 <= 0 || cb >= nb2) return;
+  const int b1 = h * NB;
+  const int64_t off1 = (int64_t)s1 * NB, off2 = (int64_t)s2 * NB;
+  const double* Ab = W + (off1 + rb * NB) * ldw + off1;           // A(m=r,k=q) = W[off1+r][off1+q]
+  const double* Bb = T + (int64_t)p * b1 * b1 + cb * NB;          // B(k=q,n=c) = T[q][c]
+  Tile tile;
+  tile.run(Ab, ldw, Bb, b1, rb * NB, b1, smem);
+  double* Wo = W + (off1 + rb * NB) * ldw + off2 + cb * NB;
+#pragma unroll
+  for (int i = 0; i < Tile::WM; ++i)
+#pragma unroll
+    for (int j = 0; j < Tile::WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Wo[(int64_t)Tile::row_of(i, r) * ldw + Tile::col_of(j)] = -tile.acc[i][j][r];
+}
+
+hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, const double* Dinv, double* W,
+                        int64_t ldw, double* T) {
+  LaunchTimer tm(c, GPX_TIMER_TRTRI);
+  const int nblk = npad / NB;
+  trtri_diag_kernel<<<nblk, WG, 0, c->stream>>>(Dinv, W, ldw);
+  for (int h = 1; h < nblk; h *= 2) {
+    const int groups = (nblk + 2 * h - 1) / (2 * h);
+    dim3 grid(h, h, groups);
+    trtri_t_kernel<<<grid, WG, 0, c->stream>>>(L, ldl, W, ldw, T, h, nblk);
+    trtri_w_kernel<<<grid, WG, 0, c->stream>>>(W, ldw, T, h, nblk);
+  }
+  return hipGetLastError();
+}
+
+// ---- alpha -----------------------------------------------------------------------------------------
+constexpr int AK = 128;  // k-chunk of the z = W^T y pass
+
+// zpart[kc][i][r] = sum_{k in chunk kc, k <= i} W[k][i] * ytil[k][r]
+__global__ void __launch_bounds__(WG) alpha_z_kernel(int n, int npad, const double* __restrict__ W, int64_t ldw,
+                                                     const double* __restrict__ Y, int64_t ldy, int nrhs,
+                                                     double const_mean, double* __restrict__ zpart) {
+  __shared__ double ys[AK][GPX_MAX_RHS];
+  const int i = blockIdx.x * WG + threadIdx.x;
+  const int kc = blockIdx.y;
+  const int k0 = kc * AK;
+  if (k0 > blockIdx.x * WG + WG - 1) return;  // whole chunk below every column of this block: unused
+  for (int e = threadIdx.x; e < AK * nrhs; e += WG) {
+    const int kk = e / nrhs, r = e % nrhs;
+    const int k = k0 + kk;
+    ys[kk][r] = (k < n) ? (Y[(int64_t)k * ldy + r] - const_mean) : 0.0;
+  }
+  __syncthreads();
+  double acc[GPX_MAX_RHS];
+#pragma unroll
+  for (int r = 0; r < GPX_MAX_RHS; ++r) acc[r] = 0.0;
+  if (i < npad) {
+    const int kend = min(k0 + AK, i + 1);
+    for (int k = k0; k < kend; ++k) {
+      const double w = W[(int64_t)k * ldw + i];
+#pragma unroll
+      for (int r = 0; r < GPX_MAX_RHS; ++r)
+        if (r < nrhs) acc[r] += w * ys[k - k0][r];
+    }
+    for (int r = 0; r < nrhs; ++r) zpart[((int64_t)kc * npad + i) * nrhs + r] = acc[r];
+  }
+}
+
+// z[i][r] = sum over valid chunks
+__global__ void __launch_bounds__(WG) alpha_zsum_kernel(int npad, int nrhs, const double* __restrict__ zpart,
+                                                        double* __restrict__ z) {
+  const int e = blockIdx.x * WG + threadIdx.x;
+  if (e >= npad * nrhs) return;
+  const int i = e / nrhs;
+  double s = 0.0;
+  for (int kc = 0; kc * AK <= i; ++kc) s += zpart[(int64_t)kc * npad * nrhs + e];
+  z[e] = s;
+}
+
+// alpha[k][r] = sum_{i >= k} W[k][i] z[i][r]; one wave per row k.
+__global__ void __launch_bounds__(WG) alpha_w_kernel(int n, int npad, const double* __restrict__ W, int64_t ldw,
+                                                     const double* __restrict__ z, int nrhs,
+                                                     double* __restrict__ alpha) {
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (k >= npad) return;
+  double acc[GPX_MAX_RHS];
+#pragma unroll
+  for (int r = 0; r < GPX_MAX_RHS; ++r) acc[r] = 0.0;
+  for (int i = k + lane; i < npad; i += 64) {
+    const double w = W[(int64_t)k * ldw + i];
+#pragma unroll
+    for (int r = 0; r < GPX_MAX_RHS; ++r)
+      if (r < nrhs) acc[r] += w * z[(int64_t)i * nrhs + r];
+  }
+#pragma unroll
+  for (int r = 0; r < GPX_MAX_RHS; ++r) {
+    if (r < nrhs) {
+      double v = acc[r];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if (lane == 0) alpha[(int64_t)k * nrhs + r] = (k < n) ? v : 0.0;
+    }
+  }
+}
+
+hipError_t launch_alpha(Context* c, int n, int npad, const double* W, int64_t ldw, const double* Y, int64_t ldy,
+                        int nrhs, double const_mean, double* alpha, double* zpart, double* z) {
+  LaunchTimer tm(c, GPX_TIMER_ALPHA);
+  dim3 g1((npad + WG - 1) / WG, npad / AK);
+  alpha_z_kernel<<<g1, WG, 0, c->stream>>>(n, npad, W, ldw, Y, ldy, nrhs, const_mean, zpart);
+  alpha_zsum_kernel<<<(npad * nrhs + WG - 1) / WG, WG, 0, c->stream>>>(npad, nrhs, zpart, z);
+  alpha_w_kernel<<<(npad + 3) / 4, WG, 0, c->stream>>>(n, npad, W, ldw, z, nrhs, alpha);
+  return hipGetLastError();
+}
+
+}  // namespace gpx

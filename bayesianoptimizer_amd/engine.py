@@ -1,0 +1,354 @@
+"""GPEngine — tensors in, tensors out, through the C ABI of libgpx.so.
+
+PyTorch-ROCm tensors are only device-memory containers here: every byte of arithmetic on the hot path
+(Gram, Cholesky, triangular inverse, alpha, K*, the triangular sweep, acquisition, argmax) runs in the
+hand-written HIP kernels of ``bayesianoptimizer_amd/csrc``.  All launches go on torch's current stream of
+the engine's device, so torch events / synchronisation compose with them.
+
+Reference surface this mirrors:
+  fit       ≙ SingleTaskGP(train_X, train_Y) + exact posterior caches (optimization/Bayesian.py:89-94,
+              optimization/Bayesian6.py:458-490) with FIXED hyperparameters (MLL fitting is §8f row 1)
+  posterior ≙ model.posterior(X).mean / .variance (optimization/Bayesian2.py:169-171,
+              optimization/Bayesian6.py:615-617)
+  acquire   ≙ analytic EI/LogEI/UCB or posterior-variance sweep + argmax (optimization/Bayesian.py:96-113,
+              optimization/Bayesian7.py:646-681)
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass, field
+from typing import Optional, Sequence, Union
+
+import torch
+
+from . import _capi
+from ._capi import (ACQ_EI, ACQ_LOGEI, ACQ_UCB, ACQ_VARIANCE, KERNEL_MATERN52, KERNEL_RBF,
+                    KERNEL_SCALE_LINEAR_MATERN52, AcqParamsC, GPXError, KernelParamsC,
+                    NotPositiveDefiniteError)
+
+KERNEL_KINDS = {"rbf": KERNEL_RBF, "matern52": KERNEL_MATERN52,
+                "scale_linear_matern52": KERNEL_SCALE_LINEAR_MATERN52}
+ACQ_KINDS = {"ei": ACQ_EI, "logei": ACQ_LOGEI, "ucb": ACQ_UCB, "variance": ACQ_VARIANCE}
+
+
+def botorch_default_lengthscale(d: int) -> float:
+    """Mode of BoTorch's dimension-scaled LogNormal(sqrt2 + log(d)/2, sqrt3) lengthscale prior [upstream]
+    (the prior of the SingleTaskGP default covariance reached from optimization/Bayesian.py:91)."""
+    return math.exp(math.sqrt(2.0) + 0.5 * math.log(d) - 3.0)
+
+
+@dataclass
+class KernelParams:
+    """Fixed GP hyperparameters (the arguments of the reference's covar_module/likelihood/mean)."""
+
+    kind: Union[str, int] = "rbf"
+    lengthscale: Union[float, Sequence[float]] = 1.0
+    outputscale: float = 1.0
+    noise: float = 1e-4
+    jitter: float = 0.0
+    const_mean: float = 0.0
+    linear_variance: Union[float, Sequence[float]] = 1.0
+
+    @property
+    def kind_id(self) -> int:
+        if isinstance(self.kind, str):
+            try:
+                return KERNEL_KINDS[self.kind.lower()]
+            except KeyError as e:
+                raise ValueError(f"unknown kernel '{self.kind}', expected one of {sorted(KERNEL_KINDS)}") from e
+        return int(self.kind)
+
+    def lengthscales(self, d: int):
+        ls = [float(self.lengthscale)] * d if isinstance(self.lengthscale, (int, float)) else \
+            [float(v) for v in self.lengthscale]
+        if len(ls) != d:
+            raise ValueError(f"expected {d} lengthscales, got {len(ls)}")
+        return ls
+
+    def linear_variances(self, d: int):
+        lv = [float(self.linear_variance)] * d if isinstance(self.linear_variance, (int, float)) else \
+            [float(v) for v in self.linear_variance]
+        if len(lv) != d:
+            raise ValueError(f"expected {d} linear variances, got {len(lv)}")
+        return lv
+
+    def to_c(self, d: int) -> KernelParamsC:
+        if not 1 <= d <= _capi.GPX_MAX_DIM:
+            raise ValueError(f"input dimension {d} outside [1, {_capi.GPX_MAX_DIM}]")
+        c = KernelParamsC()
+        c.kind = self.kind_id
+        c.d = d
+        for k, v in enumerate(self.lengthscales(d)):
+            c.lengthscale[k] = v
+        for k, v in enumerate(self.linear_variances(d)):
+            c.linear_variance[k] = v
+        c.outputscale = float(self.outputscale)
+        c.noise = float(self.noise)
+        c.jitter = float(self.jitter)
+        c.const_mean = float(self.const_mean)
+        return c
+
+    def replace(self, **kw) -> "KernelParams":
+        d = dict(self.__dict__)
+        d.update(kw)
+        return KernelParams(**d)
+
+
+@dataclass
+class GPState:
+    """Device-resident posterior caches of one exact GP (all tensors on the engine's device).
+
+    L: padded lower Cholesky factor (only its lower triangle is defined), W = L^{-T} (upper), alpha =
+    K^{-1}(Y - m) (padded_n x nrhs), Dinv: inverses of the 64x64 diagonal blocks of L.
+    """
+
+    X: torch.Tensor
+    L: torch.Tensor
+    W: torch.Tensor
+    Dinv: torch.Tensor
+    alpha: torch.Tensor
+    info: torch.Tensor
+    params: KernelParams
+    n: int
+    npad: int
+    nrhs: int
+
+    @property
+    def d(self) -> int:
+        return self.X.shape[1]
+
+    def pivot_failure(self) -> int:
+        """0-based failing pivot, or -1 (synchronises)."""
+        v = int(self.info.item())
+        return v - 1 if v else -1
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+class GPEngine:
+    """One engine per device; launches on torch's current stream of that device."""
+
+    def __init__(self, device: Union[int, str, torch.device, None] = None):
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device) if not isinstance(device, torch.device) else device
+        if device.type != "cuda":
+            raise ValueError("GPEngine runs on a ROCm GPU device ('cuda:N'); there is no CPU path")
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = device
+        self.lib = _capi.load()
+        h = ctypes.c_void_p()
+        st = self.lib.gpx_create(int(device.index), ctypes.byref(h))
+        if st != _capi.GPX_OK:
+            raise GPXError(st, f"gpx_create(device={device.index}) failed")
+        self.handle = h
+        self._ws = {}
+        self._stream_ptr = None
+
+    # -- plumbing ---------------------------------------------------------------------------------
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None) is not None and self.lib is not None:
+                self.lib.gpx_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+    def _bind_stream(self):
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        if s != self._stream_ptr:
+            _capi.check(self.lib.gpx_set_stream(self.handle, ctypes.c_void_p(s)), self.handle)
+            self._stream_ptr = s
+
+    def _check(self, st: int):
+        _capi.check(st, self.handle)
+
+    def workspace(self, key: str, nbytes: int) -> torch.Tensor:
+        buf = self._ws.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
+            self._ws[key] = buf
+        return buf
+
+    def _as_f64(self, t, name: str) -> torch.Tensor:
+        if not isinstance(t, torch.Tensor):
+            t = torch.as_tensor(t)
+        t = t.to(device=self.device, dtype=torch.float64)
+        if t.dim() == 1:
+            t = t.unsqueeze(-1)
+        return t.contiguous()
+
+    @staticmethod
+    def padded_n(n: int) -> int:
+        return ((n + _capi.GPX_TILE - 1) // _capi.GPX_TILE) * _capi.GPX_TILE
+
+    # -- fit --------------------------------------------------------------------------------------
+    def alloc_state(self, X: torch.Tensor, nrhs: int, params: KernelParams) -> GPState:
+        n = X.shape[0]
+        npad = self.padded_n(n)
+        nblk = npad // 64
+        dev = self.device
+        return GPState(
+            X=X,
+            L=torch.empty((npad, npad), dtype=torch.float64, device=dev),
+            W=torch.empty((npad, npad), dtype=torch.float64, device=dev),
+            Dinv=torch.empty((2 * nblk, 64, 64), dtype=torch.float64, device=dev),
+            alpha=torch.empty((npad, nrhs), dtype=torch.float64, device=dev),
+            info=torch.zeros((1,), dtype=torch.int32, device=dev),
+            params=params, n=n, npad=npad, nrhs=nrhs)
+
+    def fit(self, X, Y, params: KernelParams, check: bool = True, out: Optional[GPState] = None) -> GPState:
+        """One posterior update: Gram + blocked Cholesky + L^{-T} + alpha for up to 8 outputs sharing X.
+
+        With ``check`` (default) synchronises and raises NotPositiveDefiniteError like psd_safe_cholesky
+        would; with ``check=False`` stays asynchronous (inspect ``state.info`` later).
+        """
+        X = self._as_f64(X, "X")
+        Y = self._as_f64(Y, "Y")
+        n, d = X.shape
+        if Y.shape[0] != n:
+            raise ValueError(f"X has {n} rows but Y has {Y.shape[0]}")
+        nrhs = Y.shape[1]
+        if not 1 <= nrhs <= _capi.GPX_MAX_RHS:
+            raise ValueError(f"number of outputs {nrhs} outside [1, {_capi.GPX_MAX_RHS}]")
+        pc = params.to_c(d)
+        st = out if (out is not None and out.n == n and out.nrhs == nrhs) else self.alloc_state(X, nrhs, params)
+        st.X, st.params = X, params
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_fit_workspace_size(n, nrhs, ctypes.byref(nbytes)))
+        ws = self.workspace("fit", nbytes.value)
+        self._bind_stream()
+        self._check(self.lib.gpx_fit_f64(
+            self.handle, ctypes.byref(pc), n, _ptr(X), X.stride(0), _ptr(Y), Y.stride(0), nrhs,
+            _ptr(st.L), st.npad, _ptr(st.Dinv), _ptr(st.W), st.npad, _ptr(st.alpha), _ptr(st.info),
+            _ptr(ws), ws.numel()))
+        if check:
+            piv = st.pivot_failure()
+            if piv >= 0:
+                raise NotPositiveDefiniteError(piv)
+        return st
+
+    # individual stages (tests and benchmarks)
+    def gram(self, X, params: KernelParams) -> torch.Tensor:
+        X = self._as_f64(X, "X")
+        n, d = X.shape
+        npad = self.padded_n(n)
+        K = torch.zeros((npad, npad), dtype=torch.float64, device=self.device)
+        pc = params.to_c(d)
+        self._bind_stream()
+        self._check(self.lib.gpx_gram_f64(self.handle, ctypes.byref(pc), n, _ptr(X), X.stride(0), _ptr(K), npad))
+        return K
+
+    def potrf(self, K: torch.Tensor, n: int):
+        """In-place Cholesky of a padded matrix; returns (Dinv, info tensor)."""
+        npad = K.shape[0]
+        Dinv = torch.empty((2 * (npad // 64), 64, 64), dtype=torch.float64, device=self.device)
+        info = torch.zeros((1,), dtype=torch.int32, device=self.device)
+        self._bind_stream()
+        self._check(self.lib.gpx_potrf_f64(self.handle, n, _ptr(K), K.stride(0), _ptr(Dinv), _ptr(info)))
+        return Dinv, info
+
+    def trtri(self, L: torch.Tensor, Dinv: torch.Tensor, n: int) -> torch.Tensor:
+        npad = L.shape[0]
+        W = torch.zeros((npad, npad), dtype=torch.float64, device=self.device)
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_trtri_workspace_size(n, ctypes.byref(nbytes)))
+        ws = self.workspace("fit", nbytes.value)
+        self._bind_stream()
+        self._check(self.lib.gpx_trtri_f64(self.handle, n, _ptr(L), L.stride(0), _ptr(Dinv), _ptr(W), npad,
+                                           _ptr(ws), ws.numel()))
+        return W
+
+    # -- posterior / acquisition ----------------------------------------------------------------
+    def posterior(self, state: GPState, Xs, y_mean: Optional[Sequence[float]] = None,
+                  y_scale: Optional[Sequence[float]] = None):
+        """Posterior mean (m x nrhs) and variance (m) at Xs; (y_mean, y_scale) = Standardize untransform."""
+        Xs = self._as_f64(Xs, "Xs")
+        if Xs.shape[1] != state.d:
+            raise ValueError(f"Xs has {Xs.shape[1]} columns, model has d={state.d}")
+        m = Xs.shape[0]
+        mean = torch.empty((m, state.nrhs), dtype=torch.float64, device=self.device)
+        var = torch.empty((m,), dtype=torch.float64, device=self.device)
+        if m == 0:
+            return mean, var
+        ym = (ctypes.c_double * state.nrhs)(*([0.0] * state.nrhs if y_mean is None else [float(v) for v in y_mean]))
+        ys = (ctypes.c_double * state.nrhs)(*([1.0] * state.nrhs if y_scale is None else [float(v) for v in y_scale]))
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_sweep_workspace_size(state.n, state.nrhs, m, ctypes.byref(nbytes)))
+        ws = self.workspace("sweep", nbytes.value)
+        pc = state.params.to_c(state.d)
+        self._bind_stream()
+        self._check(self.lib.gpx_posterior_f64(
+            self.handle, ctypes.byref(pc), state.n, _ptr(state.X), state.X.stride(0), _ptr(state.W), state.npad,
+            _ptr(state.alpha), state.nrhs, _ptr(Xs), m, Xs.stride(0), ym, ys, _ptr(mean), state.nrhs, _ptr(var),
+            _ptr(ws), ws.numel()))
+        return mean, var
+
+    def acquire(self, state: GPState, Xs, kind: Union[str, int] = "logei", best_f: float = 0.0, beta: float = 4.0,
+                y_mean: float = 0.0, y_scale: float = 1.0, alpha: Optional[torch.Tensor] = None,
+                index_offset: int = 0, return_scores: bool = False):
+        """Score every candidate and return device scalars (best_value, best_index) (+ scores)."""
+        Xs = self._as_f64(Xs, "Xs")
+        if Xs.shape[1] != state.d:
+            raise ValueError(f"Xs has {Xs.shape[1]} columns, model has d={state.d}")
+        m = Xs.shape[0]
+        if m == 0:
+            raise ValueError("empty candidate set")
+        kid = ACQ_KINDS[kind.lower()] if isinstance(kind, str) else int(kind)
+        if alpha is None:
+            alpha = state.alpha[:, 0]
+        alpha = alpha.to(device=self.device, dtype=torch.float64).contiguous()
+        if alpha.numel() != state.npad:
+            raise ValueError("alpha must have padded_n entries")
+        ap = AcqParamsC()
+        ap.kind, ap.best_f, ap.beta, ap.y_mean, ap.y_scale = kid, float(best_f), float(beta), float(y_mean), \
+            float(y_scale)
+        best_val = torch.empty((1,), dtype=torch.float64, device=self.device)
+        best_idx = torch.empty((1,), dtype=torch.int64, device=self.device)
+        scores = torch.empty((m,), dtype=torch.float64, device=self.device) if return_scores else None
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_sweep_workspace_size(state.n, 1, m, ctypes.byref(nbytes)))
+        ws = self.workspace("sweep", nbytes.value)
+        pc = state.params.to_c(state.d)
+        self._bind_stream()
+        self._check(self.lib.gpx_acquire_argmax_f64(
+            self.handle, ctypes.byref(pc), state.n, _ptr(state.X), state.X.stride(0), _ptr(state.W), state.npad,
+            _ptr(alpha), _ptr(Xs), m, Xs.stride(0), ctypes.byref(ap), int(index_offset), _ptr(best_val),
+            _ptr(best_idx), _ptr(scores), _ptr(ws), ws.numel()))
+        if return_scores:
+            return best_val, best_idx, scores
+        return best_val, best_idx
+
+    def argmax_combine(self, vals: torch.Tensor, idx: torch.Tensor):
+        """Deterministic (max value, lowest index) over device records (after the cross-rank gather)."""
+        vals = vals.to(device=self.device, dtype=torch.float64).contiguous().reshape(-1)
+        idx = idx.to(device=self.device, dtype=torch.int64).contiguous().reshape(-1)
+        bv = torch.empty((1,), dtype=torch.float64, device=self.device)
+        bi = torch.empty((1,), dtype=torch.int64, device=self.device)
+        self._bind_stream()
+        self._check(self.lib.gpx_argmax_combine_f64(self.handle, _ptr(vals), _ptr(idx), vals.numel(), _ptr(bv),
+                                                    _ptr(bi)))
+        return bv, bi
+
+    # -- instrumentation ------------------------------------------------------------------------
+    def timing_enable(self, timers: Sequence[str] = ("trmm",)):
+        mask = 0
+        for t in timers:
+            mask |= 1 << _capi.TIMERS[t]
+        self._check(self.lib.gpx_timing_enable(self.handle, mask))
+
+    def timing_disable(self):
+        self._check(self.lib.gpx_timing_enable(self.handle, 0))
+
+    def timing_reset(self):
+        self._check(self.lib.gpx_timing_reset(self.handle))
+
+    def timing_query(self, timer: str):
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        self._check(self.lib.gpx_timing_query(self.handle, _capi.TIMERS[timer], ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value

@@ -1,0 +1,176 @@
+/*
+ * gpx.h — C ABI of the MI355X-native exact-GP posterior engine (libgpx.so).
+ *
+ * This is the drop-in boundary for the hot path of billbearhunter/BayesianOptimizer.  In the reference
+ * the path runs inside BoTorch/GPyTorch (not vendored); each entry point below names the reference call
+ * site whose arithmetic it replaces.  Python binds it with ctypes (bayesianoptimizer_amd/_capi.py); see
+ * INTEGRATION.md for the binding stub a maintainer adds to the reference.
+ *
+ * Conventions
+ *  - Every array pointer is a DEVICE pointer owned by the caller (PyTorch tensors serve as containers).
+ *    Host pointers are only the parameter structs and the out-scalars named *_host.
+ *  - All matrices are row-major fp64 with an explicit leading dimension (in elements).
+ *  - Training size n is padded internally to gpx_padded_n(n) (a multiple of GPX_TILE); padded rows of K are
+ *    the identity, so L, L^{-1} and alpha are exact block extensions of the unpadded ones.  Buffers named
+ *    "padded" must have gpx_padded_n(n) rows/cols.
+ *  - Calls are asynchronous on the handle's stream (gpx_set_stream) and never allocate device memory;
+ *    scratch comes from the caller's workspace (size from the *_workspace_size queries).
+ *  - Errors: return a gpx_status; gpx_last_error(h) gives a message.  NOT_PD is reported through a device
+ *    int32 `info` (0 = OK, else failing pivot + 1, LAPACK potrf convention) so the fit stays asynchronous;
+ *    gpx_fit_f64_sync reads it back and returns GPX_NOT_PD, like the reference's jitter-retry path
+ *    (optimization/Bayesian6.py:481-488) expects an exception.
+ */
+#ifndef GPX_H
+#define GPX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPX_MAX_DIM 32
+#define GPX_MAX_RHS 8
+#define GPX_TILE 128
+
+typedef struct gpx_context* gpx_handle;
+typedef int32_t gpx_status;
+
+enum {
+  GPX_OK = 0,
+  GPX_NOT_PD = 1,
+  GPX_INVALID_ARG = 2,
+  GPX_HIP_ERROR = 3,
+  GPX_RCCL_ERROR = 4
+};
+
+/* Covariance modules used by the reference.
+ * RBF: BoTorch SingleTaskGP default (optimization/Bayesian.py:91, Bayesian1.py:109) [upstream]
+ * MATERN52: MaternKernel(nu=2.5) (config 3 of BASELINE.json)
+ * SCALE_LINEAR_MATERN52: ScaleKernel(LinearKernel + MaternKernel(2.5)) (optimization/Bayesian6.py:471-473,
+ *                        optimization/Bayesian7.py:162-166) */
+enum { GPX_KERNEL_RBF = 0, GPX_KERNEL_MATERN52 = 1, GPX_KERNEL_SCALE_LINEAR_MATERN52 = 2 };
+
+/* Acquisition scores (maximised). EI/LOGEI/UCB: BoTorch analytic forms [upstream] of the qLogEI call
+ * (optimization/Bayesian.py:100-101); VARIANCE: the pool-scan score of optimization/Bayesian7.py:671. */
+enum { GPX_ACQ_EI = 0, GPX_ACQ_LOGEI = 1, GPX_ACQ_UCB = 2, GPX_ACQ_VARIANCE = 3 };
+
+/* Timers kept by gpx_timing_* (one per kernel family; gpx_timing_enable takes a bitmask of 1<<timer). */
+enum {
+  GPX_TIMER_GRAM = 0,
+  GPX_TIMER_POTRF = 1,
+  GPX_TIMER_TRTRI = 2,
+  GPX_TIMER_ALPHA = 3,
+  GPX_TIMER_KSTAR = 4,
+  GPX_TIMER_TRMM = 5,
+  GPX_TIMER_ACQ = 6,
+  GPX_TIMER_COUNT = 7
+};
+
+typedef struct {
+  int32_t kind;                          /* GPX_KERNEL_* */
+  int32_t d;                             /* input dimension, 1..GPX_MAX_DIM */
+  double lengthscale[GPX_MAX_DIM];       /* ARD lengthscales (Matérn / RBF part) */
+  double linear_variance[GPX_MAX_DIM];   /* ARD LinearKernel variances (SCALE_LINEAR_MATERN52 only) */
+  double outputscale;                    /* ScaleKernel s^2 (1.0 for BoTorch>=0.12 RBF default) */
+  double noise;                          /* GaussianLikelihood noise sigma^2 */
+  double jitter;                         /* extra diagonal (gpytorch.settings.cholesky_jitter) */
+  double const_mean;                     /* ConstantMean */
+} gpx_kernel_params;
+
+typedef struct {
+  int32_t kind;     /* GPX_ACQ_* */
+  int32_t reserved;
+  double best_f;    /* incumbent, in untransformed units (optimization/Bayesian.py:98) */
+  double beta;      /* UCB beta */
+  double y_mean;    /* Standardize untransform: mu_out = y_mean + y_scale * mu */
+  double y_scale;   /*                          var_out = y_scale^2 * var       */
+} gpx_acq_params;
+
+/* ---- library / handle ---------------------------------------------------------------------------- */
+const char* gpx_version(void);
+gpx_status gpx_create(int32_t device, gpx_handle* out);
+gpx_status gpx_destroy(gpx_handle h);
+/* stream: a hipStream_t passed as void* (NULL = default stream). */
+gpx_status gpx_set_stream(gpx_handle h, void* stream);
+const char* gpx_last_error(gpx_handle h);
+int64_t gpx_padded_n(int64_t n);
+
+/* ---- fit = posterior update ----------------------------------------------- */
+/* Gram K(X,X)+(noise+jitter)I into the lower triangle of the padded K (replaces the covar_module(X) +
+ * likelihood evaluation inside ExactMarginalLogLikelihood / ExactGP prediction strategy [upstream],
+ * reached from optimization/Bayesian.py:91-93 and optimization/Bayesian6.py:476-484). */
+gpx_status gpx_gram_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                        double* K, int64_t ldk);
+
+/* In-place blocked lower Cholesky of the padded matrix (replaces psd_safe_cholesky [upstream];
+ * jitter policy optimization/Bayesian6.py:483,487).  Dinv (2 * padded_n/64 * 64*64 doubles) receives the
+ * inverses of the 64x64 diagonal blocks in its first half; the second half is scratch.  Only the lower
+ * triangle of A is defined afterwards.  info: device int32, 0 or pivot+1. */
+gpx_status gpx_potrf_f64(gpx_handle h, int64_t n, double* A, int64_t lda, double* Dinv, int32_t* info);
+
+/* W = L^{-T} (upper triangular, row-major, i.e. W[k][i] = (L^{-1})[i][k]; strict lower part zeroed).
+ * Needs the Dinv of gpx_potrf_f64.  Used by alpha and the candidate sweep. */
+gpx_status gpx_trtri_workspace_size(int64_t n, size_t* bytes);
+gpx_status gpx_trtri_f64(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv, double* W,
+                         int64_t ldw, void* ws, size_t ws_bytes);
+
+/* alpha = K^{-1} (Y - const_mean) = W W^T (Y - m) for nrhs <= GPX_MAX_RHS right-hand sides.  Y: n x nrhs
+ * row-major with leading dim ldy; alpha: contiguous padded_n x nrhs (rows >= n are set to 0).
+ * Replaces the ExactGP mean_cache [upstream]. */
+gpx_status gpx_alpha_workspace_size(int64_t n, int64_t nrhs, size_t* bytes);
+gpx_status gpx_alpha_f64(gpx_handle h, int64_t n, const double* W, int64_t ldw, const double* Y, int64_t ldy,
+                         int64_t nrhs, double const_mean, double* alpha, void* ws, size_t ws_bytes);
+
+/* One full posterior update: Gram + Cholesky + L^{-T} + alpha.  K (padded, in/out: holds L afterwards),
+ * W, Dinv, alpha as above.  Asynchronous; *info (device) reports NOT_PD. */
+gpx_status gpx_fit_workspace_size(int64_t n, int64_t nrhs, size_t* bytes);
+gpx_status gpx_fit_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                       const double* Y, int64_t ldy, int64_t nrhs, double* K, int64_t ldk, double* Dinv,
+                       double* W, int64_t ldw, double* alpha, int32_t* info, void* ws, size_t ws_bytes);
+/* Same, then synchronises the stream and returns GPX_NOT_PD with *info_host = pivot+1 on failure. */
+gpx_status gpx_fit_f64_sync(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                            const double* Y, int64_t ldy, int64_t nrhs, double* K, int64_t ldk, double* Dinv,
+                            double* W, int64_t ldw, double* alpha, int32_t* info, void* ws, size_t ws_bytes,
+                            int32_t* info_host);
+
+/* ---- posterior / acquisition ---------------------------------------------- */
+/* Posterior at m points Xs (m x d, ld ldxs): mean (m x nrhs, ld ldmean) and variance (m), untransformed
+ * by (y_mean[r], y_scale[r]) per output r (host arrays of nrhs; NULL = identity).  Replaces
+ * model.posterior(X).mean/.variance (optimization/Bayesian2.py:169-171, optimization/Bayesian6.py:615-617).
+ * var_out is the variance of output 0's untransform (all outputs share the factor). */
+gpx_status gpx_sweep_workspace_size(int64_t n, int64_t nrhs, int64_t m, size_t* bytes);
+gpx_status gpx_posterior_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                             const double* W, int64_t ldw, const double* alpha, int64_t nrhs, const double* Xs,
+                             int64_t m, int64_t ldxs, const double* y_mean_host, const double* y_scale_host,
+                             double* mean_out, int64_t ldmean, double* var_out, void* ws, size_t ws_bytes);
+
+/* Candidate sweep: score m candidates with an analytic acquisition on the posterior whose mean uses the
+ * padded_n vector `alpha` (one output column of gpx_alpha_f64, or a weighted combination of columns for a
+ * linear objective) and reduce to (best value, lowest index among ties); reported indices are
+ * index_offset + local index (candidate shards on several GPUs).  best_val/best_idx are device scalars; scores_out
+ * (device, m) is optional (NULL = not written).  Replaces the raw-sample sweep + argmax of optimize_acqf
+ * (optimization/Bayesian.py:105-113) and the pool scan + topk of optimization/Bayesian7.py:646-681. */
+gpx_status gpx_acquire_argmax_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X,
+                                  int64_t ldx, const double* W, int64_t ldw, const double* alpha,
+                                  const double* Xs, int64_t m, int64_t ldxs, const gpx_acq_params* a,
+                                  int64_t index_offset, double* best_val, int64_t* best_idx,
+                                  double* scores_out, void* ws, size_t ws_bytes);
+
+/* Deterministic (value, index) reduction of `count` device records: max value, then lowest index; NaN
+ * never wins.  Used after the cross-GPU all-gather of per-rank records. */
+gpx_status gpx_argmax_combine_f64(gpx_handle h, const double* vals, const int64_t* idx, int64_t count,
+                                  double* best_val, int64_t* best_idx);
+
+/* ---- instrumentation ------------------------------------------------------------------------------ */
+/* For every timer whose bit is set in `mask`, each launch of that kernel family is bracketed by hipEvents
+ * on the handle's stream; totals are read with gpx_timing_query (synchronises the stream). mask 0 = off. */
+gpx_status gpx_timing_enable(gpx_handle h, int32_t mask);
+gpx_status gpx_timing_reset(gpx_handle h);
+gpx_status gpx_timing_query(gpx_handle h, int32_t timer, double* total_ms_host, int64_t* launches_host);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPX_H */

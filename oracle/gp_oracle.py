@@ -1,0 +1,328 @@
+"""CPU oracle for the exact-GP posterior hot path — TEST INFRASTRUCTURE ONLY.
+
+This module is the checker, never the product: only ``tests/``, ``__graft_entry__.smoke()`` and
+``bench.py``'s ``cpu_baseline`` leg may import it.  The shipped path (``bayesianoptimizer_amd``)
+never imports anything under ``oracle/`` and fails loudly when its HIP library is missing.
+
+What it restates (fp64, NumPy/SciPy):
+
+* a3  Gram build ``K(X,X) + (noise + jitter) I`` for the three kernels the reference uses:
+      RBF (BoTorch >= 0.12 ``SingleTaskGP`` default covariance, reached from
+      ``optimization/Bayesian.py:91`` and ``optimization/Bayesian1.py:109``), Matérn-5/2, and
+      ``ScaleKernel(LinearKernel + MaternKernel(nu=2.5))`` (``optimization/Bayesian6.py:471-473``,
+      ``optimization/Bayesian7.py:162-166``).  [upstream] GPyTorch kernel formulas.
+* a4  Cholesky ``K = L L^T`` with NOT_PD reporting of the failing pivot (the reference retries
+      with a larger jitter, ``optimization/Bayesian6.py:481-488``).
+* a5  ``alpha = K^{-1} (y - m)``, m = ConstantMean.
+* a6  Posterior ``mu = m + k*^T alpha``, ``var = k** - ||L^{-1} k*||^2`` with GPyTorch's
+      double-precision variance floor (1e-10) and BoTorch's ``min_var`` floor (1e-12), as used by
+      ``model.posterior(X).mean/.variance`` (``optimization/Bayesian2.py:169-171``,
+      ``optimization/Bayesian6.py:615-617``).
+* a7  Analytic EI / LogEI / UCB / posterior-variance scores (BoTorch analytic acquisition
+      formulas [upstream]; the reference's qLogEI call site is ``optimization/Bayesian.py:100-101``,
+      the variance-sum pool scan is ``optimization/Bayesian7.py:664-671``).
+* a8  Argmax with the lowest index winning ties (``optimization/Bayesian.py:117``,
+      ``optimization/Bayesian7.py:681,724-727``).
+* a1/a2 input/output transforms of ``optimization/Bayesian7.py:181-190,363-385``.
+
+Parity status: **parity unpinned**.  The reference delegates this arithmetic to GPyTorch /
+BoTorch / linear_operator, which are not installed here and not vendored under the reference,
+and the reference holds no tests or golden vectors for this path.  The
+oracle is therefore pinned by closed-form known-answer tests (tests/test_oracle.py) and by the
+golden fixtures it generates itself (tests/golden/make_golden.py); parity is defined against the
+exact-Cholesky formulation (no CG/Lanczos/LOVE, no MC sampling), see DESIGN.md §3.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+import scipy.linalg as sla
+from scipy.special import erfcx, ndtr
+
+RBF = 0
+MATERN52 = 1
+SCALE_LINEAR_MATERN52 = 2
+
+ACQ_EI = 0
+ACQ_LOGEI = 1
+ACQ_UCB = 2
+ACQ_VARIANCE = 3
+
+# GPyTorch settings.min_variance for float64 [upstream]; BoTorch analytic min_var [upstream].
+GPYTORCH_MIN_VAR_F64 = 1e-10
+BOTORCH_MIN_VAR = 1e-12
+
+
+@dataclass
+class KernelParams:
+    """Fixed GP hyperparameters (mirrors bayesianoptimizer_amd.KernelParams)."""
+
+    kind: int
+    lengthscale: np.ndarray
+    outputscale: float = 1.0
+    noise: float = 1e-4
+    const_mean: float = 0.0
+    linear_variance: Optional[np.ndarray] = None
+    jitter: float = 0.0
+
+    def __post_init__(self):
+        self.lengthscale = np.asarray(self.lengthscale, dtype=np.float64).reshape(-1)
+        if self.linear_variance is None:
+            self.linear_variance = np.ones_like(self.lengthscale)
+        self.linear_variance = np.asarray(self.linear_variance, dtype=np.float64).reshape(-1)
+        if self.linear_variance.size == 1 and self.lengthscale.size > 1:
+            self.linear_variance = np.full_like(self.lengthscale, self.linear_variance[0])
+
+
+def botorch_default_lengthscale(d: int) -> float:
+    """Mode of BoTorch's dimension-scaled LogNormal(sqrt2 + 0.5 log d, sqrt3) prior [upstream]."""
+    return math.exp(math.sqrt(2.0) + 0.5 * math.log(d) - 3.0)
+
+
+# ---------------------------------------------------------------------------------------------
+# a3: kernels
+# ---------------------------------------------------------------------------------------------
+def _sqdist_scaled(X1: np.ndarray, X2: np.ndarray, ls: np.ndarray) -> np.ndarray:
+    """Squared distances of lengthscale-scaled inputs, difference form sum_k ((a_k-b_k)/l_k)^2.
+
+    The GPU Gram/K* kernels accumulate the same per-dimension terms in the same order (k = 0..d-1),
+    so the two agree to rounding of the final exp.  [upstream] GPyTorch uses the expanded form
+    ||a||^2+||b||^2-2a.b on mean-centred inputs; that differs by O(eps) and is documented in
+    DESIGN.md as part of the parity definition.
+    """
+    A = X1 / ls
+    B = X2 / ls
+    out = np.zeros((A.shape[0], B.shape[0]), dtype=np.float64)
+    for k in range(A.shape[1]):
+        diff = A[:, k:k + 1] - B[None, :, k]
+        out += diff * diff
+    return out
+
+
+def kernel_matrix(X1: np.ndarray, X2: np.ndarray, p: KernelParams) -> np.ndarray:
+    """k(X1, X2) without noise.  Formulas per GPyTorch RBFKernel/MaternKernel/LinearKernel/ScaleKernel."""
+    X1 = np.asarray(X1, dtype=np.float64)
+    X2 = np.asarray(X2, dtype=np.float64)
+    r2 = _sqdist_scaled(X1, X2, p.lengthscale)
+    if p.kind == RBF:
+        return p.outputscale * np.exp(-0.5 * r2)
+    r = np.sqrt(r2)
+    s5r = math.sqrt(5.0) * r
+    matern = (1.0 + s5r + (5.0 / 3.0) * r2) * np.exp(-s5r)
+    if p.kind == MATERN52:
+        return p.outputscale * matern
+    if p.kind == SCALE_LINEAR_MATERN52:
+        lin = (X1 * p.linear_variance) @ X2.T
+        return p.outputscale * (lin + matern)
+    raise ValueError(f"unknown kernel kind {p.kind}")
+
+
+def kernel_diag(X: np.ndarray, p: KernelParams) -> np.ndarray:
+    """k(x, x) for each row."""
+    X = np.asarray(X, dtype=np.float64)
+    if p.kind in (RBF, MATERN52):
+        return np.full(X.shape[0], p.outputscale)
+    lin = (X * X * p.linear_variance).sum(axis=1)
+    return p.outputscale * (lin + 1.0)
+
+
+def gram(X: np.ndarray, p: KernelParams) -> np.ndarray:
+    """K(X,X) + (noise + jitter) I  (SURVEY §8a row a3)."""
+    K = kernel_matrix(X, X, p)
+    K[np.diag_indices_from(K)] += p.noise + p.jitter
+    return K
+
+
+# ---------------------------------------------------------------------------------------------
+# a4/a5: factorisation and alpha
+# ---------------------------------------------------------------------------------------------
+class NotPDError(np.linalg.LinAlgError):
+    def __init__(self, pivot: int):
+        super().__init__(f"matrix not positive definite at pivot {pivot}")
+        self.pivot = pivot
+
+
+def cholesky(K: np.ndarray) -> np.ndarray:
+    """Lower Cholesky factor; raises NotPDError(pivot) like the C-ABI's info = pivot + 1."""
+    try:
+        return sla.cholesky(K, lower=True, check_finite=False)
+    except np.linalg.LinAlgError as e:  # scipy: "%d-th leading minor not positive definite"
+        msg = str(e)
+        piv = -1
+        for tok in msg.split():
+            if tok.rstrip("-th").isdigit():
+                piv = int(tok.rstrip("-th")) - 1
+                break
+        raise NotPDError(piv) from e
+
+
+@dataclass
+class GPState:
+    X: np.ndarray
+    L: np.ndarray
+    alpha: np.ndarray  # (n,) or (n, T)
+    params: KernelParams
+
+
+def fit(X: np.ndarray, y: np.ndarray, p: KernelParams) -> GPState:
+    """One posterior update: Gram + Cholesky + alpha."""
+    X = np.asarray(X, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64)
+    K = gram(X, p)
+    L = cholesky(K)
+    alpha = sla.cho_solve((L, True), y - p.const_mean, check_finite=False)
+    return GPState(X=X, L=L, alpha=alpha, params=p)
+
+
+# ---------------------------------------------------------------------------------------------
+# a6: posterior
+# ---------------------------------------------------------------------------------------------
+def posterior(state: GPState, Xs: np.ndarray, y_mean: float = 0.0, y_scale: float = 1.0):
+    """Posterior mean/variance at Xs, untransformed by (y_mean, y_scale) like Standardize.
+
+    Variance floor order: GPyTorch clamps the standardized predictive variance at 1e-10 (double),
+    Standardize.untransform multiplies by y_scale^2, then BoTorch clamps at 1e-12 [upstream].
+    """
+    p = state.params
+    Ks = kernel_matrix(state.X, Xs, p)  # (n, m)
+    mu = p.const_mean + Ks.T @ state.alpha
+    V = sla.solve_triangular(state.L, Ks, lower=True, check_finite=False)
+    var = kernel_diag(Xs, p) - np.einsum("ij,ij->j", V, V)
+    var = np.maximum(var, GPYTORCH_MIN_VAR_F64)
+    mu = y_mean + y_scale * mu
+    var = np.maximum(var * (y_scale * y_scale), BOTORCH_MIN_VAR)
+    return mu, var
+
+
+# ---------------------------------------------------------------------------------------------
+# a7: analytic acquisition (BoTorch analytic forms, restated)
+# ---------------------------------------------------------------------------------------------
+_LOG_SQRT_2PI = 0.5 * math.log(2.0 * math.pi)
+_LOG_SQRT_PI_DIV_2 = 0.5 * math.log(math.pi / 2.0)
+_INV_SQRT_2 = 1.0 / math.sqrt(2.0)
+_NEG_INV_SQRT_EPS_F64 = -1.0 / math.sqrt(np.finfo(np.float64).eps)
+
+
+def _phi(u):
+    return np.exp(-0.5 * u * u) / math.sqrt(2.0 * math.pi)
+
+
+def _Phi(u):
+    return ndtr(u)
+
+
+def _log1mexp(x):
+    """log(1 - exp(x)) for x < 0 (Maechler's two-branch form)."""
+    x = np.asarray(x, dtype=np.float64)
+    return np.where(x > -math.log(2.0), np.log(-np.expm1(np.minimum(x, -1e-300))),
+                    np.log1p(-np.exp(np.minimum(x, 0.0))))
+
+
+def ei_helper(u):
+    return _phi(u) + u * _Phi(u)
+
+
+def log_ei_helper(u):
+    """log(phi(u) + u Phi(u)), stable for very negative u (two-branch form, bound = -1)."""
+    u = np.asarray(u, dtype=np.float64)
+    upper = np.log(ei_helper(np.maximum(u, -1.0)))
+    u_lo = np.minimum(u, -1.0)
+    u_eps = np.maximum(u_lo, _NEG_INV_SQRT_EPS_F64)
+    w = np.log(erfcx(-u_eps * _INV_SQRT_2) * np.abs(u_eps)) + _LOG_SQRT_PI_DIV_2
+    log_phi = -0.5 * u * u - _LOG_SQRT_2PI
+    lower = log_phi + np.where(u > _NEG_INV_SQRT_EPS_F64, _log1mexp(w), -2.0 * np.log(np.abs(u_lo)))
+    return np.where(u > -1.0, upper, lower)
+
+
+def acquisition(mu, var, kind: int, best_f: float = 0.0, beta: float = 4.0):
+    """Score per candidate; higher is better (maximisation)."""
+    mu = np.asarray(mu, dtype=np.float64)
+    var = np.asarray(var, dtype=np.float64)
+    sigma = np.sqrt(var)
+    if kind == ACQ_EI:
+        u = (mu - best_f) / sigma
+        return sigma * ei_helper(u)
+    if kind == ACQ_LOGEI:
+        u = (mu - best_f) / sigma
+        return log_ei_helper(u) + np.log(sigma)
+    if kind == ACQ_UCB:
+        return mu + math.sqrt(beta) * sigma
+    if kind == ACQ_VARIANCE:
+        return var
+    raise ValueError(f"unknown acquisition {kind}")
+
+
+# ---------------------------------------------------------------------------------------------
+# a8: argmax (lowest index wins ties; NaN never wins)
+# ---------------------------------------------------------------------------------------------
+def argmax_lowest(scores: np.ndarray):
+    s = np.asarray(scores, dtype=np.float64)
+    s = np.where(np.isnan(s), -np.inf, s)
+    idx = int(np.argmax(s))  # numpy returns the first occurrence of the max
+    return float(s[idx]), idx
+
+
+def acquire_argmax(state: GPState, Xs: np.ndarray, kind: int, best_f: float = 0.0,
+                   beta: float = 4.0, y_mean: float = 0.0, y_scale: float = 1.0,
+                   chunk: int = 8192):
+    """Candidate sweep + argmax.  Returns (best_value, best_index, scores)."""
+    scores = np.empty(Xs.shape[0], dtype=np.float64)
+    for s in range(0, Xs.shape[0], chunk):
+        mu, var = posterior(state, Xs[s:s + chunk], y_mean, y_scale)
+        scores[s:s + chunk] = acquisition(mu, var, kind, best_f, beta)
+    v, i = argmax_lowest(scores)
+    return v, i, scores
+
+
+def combine_argmax(records: Sequence[tuple]):
+    """Deterministic reduction of (value, global_index) records: max value, then lowest index."""
+    best = (-np.inf, np.iinfo(np.int64).max)
+    for v, i in records:
+        v = -np.inf if np.isnan(v) else v
+        if v > best[0] or (v == best[0] and i < best[1]):
+            best = (v, i)
+    return best
+
+
+# ---------------------------------------------------------------------------------------------
+# a1/a2: transforms (optimization/Bayesian7.py:181-190, 363-385)
+# ---------------------------------------------------------------------------------------------
+def log_standardize_inputs(X_unit, bounds, mean=None, std=None, std_floor=1e-6):
+    b = np.asarray(bounds, dtype=np.float64)
+    lo, hi = b[:, 0], b[:, 1]
+    X_phys = X_unit * (hi - lo) + lo
+    X_log = np.log(np.maximum(X_phys, 1e-6))
+    if mean is None:
+        mean = X_log.mean(axis=0, keepdims=True)
+        std = np.maximum(X_log.std(axis=0, ddof=1, keepdims=True), std_floor)
+    return (X_log - mean) / std, mean, std
+
+
+def standardize(Y):
+    """BoTorch Standardize: (y - mean) / std with unbiased std [upstream]."""
+    Y = np.asarray(Y, dtype=np.float64)
+    m = Y.mean(axis=0)
+    s = Y.std(axis=0, ddof=1)
+    s = np.where(s >= 1e-8, s, 1.0)
+    return (Y - m) / s, m, s
+
+
+# ---------------------------------------------------------------------------------------------
+# synthetic workload of SURVEY §8d
+# ---------------------------------------------------------------------------------------------
+def synthetic_problem(n: int, d: int, seed: int, noise_sd: float = 0.01):
+    rng = np.random.default_rng(seed)
+    X = rng.random((n, d))
+    y = np.sin(6.0 * X).sum(axis=1) + noise_sd * rng.standard_normal(n)
+    y = (y - y.mean()) / y.std()
+    return X, y
+
+
+def sobol_candidates(m: int, d: int, seed: int):
+    from scipy.stats import qmc
+    eng = qmc.Sobol(d, scramble=True, seed=seed)
+    k = int(math.ceil(math.log2(max(m, 1))))
+    return eng.random_base2(k)[:m]
