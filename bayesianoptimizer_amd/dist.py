@@ -1,0 +1,100 @@
+"""Multi-GPU sharding of independent GP problems, one process per GPU.
+
+Independent units — restarts / seeds / outputs (BASELINE configs[3]: 32 x n=4096 over 8 GPUs) or contiguous
+candidate shards of one large sweep — are partitioned in contiguous blocks across ranks; every rank fits
+and sweeps its own units with no data-path collective.  The single exchange is one 16-byte
+(fp64 value, int64 global index) record per rank, all-gathered over RCCL (torch.distributed "nccl") and
+reduced deterministically (max value, then lowest global index) by the engine's argmax_combine kernel.
+RCCL has no MAXLOC op, hence gather + local reduce instead of an all-reduce.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(total: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous block partition: rank r gets [start, stop) with sizes differing by at most one."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("invalid rank/world")
+    q, r = divmod(total, world)
+    start = rank * q + min(rank, r)
+    return start, start + q + (1 if rank < r else 0)
+
+
+def combine_records_host(vals: torch.Tensor, idx: torch.Tensor) -> Tuple[float, int]:
+    """Host reduction with the same order as the device kernel (used for CPU/gloo paths and tests)."""
+    best_v, best_i = float("-inf"), None
+    for v, i in zip(vals.reshape(-1).tolist(), idx.reshape(-1).tolist()):
+        if v != v:  # NaN never wins
+            v = float("-inf")
+        if best_i is None or v > best_v or (v == best_v and i < best_i):
+            best_v, best_i = v, i
+    return best_v, best_i
+
+
+def exchange_argmax(val: torch.Tensor, idx: torch.Tensor, engine=None, group=None):
+    """All-gather every rank's (value, global index) record and reduce it.
+
+    On GPU tensors with the nccl backend this is RCCL over xGMI and the reduction runs in the engine's
+    argmax_combine kernel; with gloo (CPU tests) the reduction is the identical host loop.
+    Returns (value, index) as 1-element tensors on val's device.
+    """
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    val = val.reshape(1).to(torch.float64)
+    idx = idx.reshape(1).to(torch.int64)
+    if world == 1:
+        gv, gi = val, idx
+    else:
+        gv = torch.empty(world, dtype=torch.float64, device=val.device)
+        gi = torch.empty(world, dtype=torch.int64, device=idx.device)
+        if val.is_cuda:
+            dist.all_gather_into_tensor(gv, val, group=group)
+            dist.all_gather_into_tensor(gi, idx, group=group)
+        else:
+            lv = [torch.empty(1, dtype=torch.float64) for _ in range(world)]
+            li = [torch.empty(1, dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(lv, val, group=group)
+            dist.all_gather(li, idx, group=group)
+            gv, gi = torch.cat(lv), torch.cat(li)
+    if engine is not None and gv.is_cuda:
+        return engine.argmax_combine(gv, gi)
+    v, i = combine_records_host(gv, gi)
+    return (torch.tensor([v], dtype=torch.float64, device=val.device),
+            torch.tensor([i], dtype=torch.int64, device=val.device))
+
+
+def sharded_best(num_units: int, local_best: Callable[[int], Tuple[torch.Tensor, torch.Tensor]],
+                 engine=None, group=None):
+    """Run ``local_best(unit)`` for this rank's contiguous share of ``num_units`` independent problems;
+    each returns (value, global_index) for its unit.  Reduce locally, then across ranks.
+
+    Returns (value, index, unit_results) where unit_results lists this rank's (unit, value, index).
+    """
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    start, stop = shard_range(num_units, rank, world)
+    vals: List[torch.Tensor] = []
+    idxs: List[torch.Tensor] = []
+    results = []
+    for u in range(start, stop):
+        v, i = local_best(u)
+        vals.append(v.reshape(1).to(torch.float64))
+        idxs.append(i.reshape(1).to(torch.int64))
+        results.append((u, v, i))
+    if vals:
+        lv, li = torch.cat(vals), torch.cat(idxs)
+        if engine is not None and lv.is_cuda:
+            bv, bi = engine.argmax_combine(lv, li)
+        else:
+            v, i = combine_records_host(lv, li)
+            bv = torch.tensor([v], dtype=torch.float64, device=lv.device)
+            bi = torch.tensor([i], dtype=torch.int64, device=lv.device)
+    else:  # more ranks than units
+        dev = torch.device("cuda", torch.cuda.current_device()) if engine is not None else torch.device("cpu")
+        bv = torch.tensor([float("-inf")], dtype=torch.float64, device=dev)
+        bi = torch.tensor([2 ** 63 - 1], dtype=torch.int64, device=dev)
+    v, i = exchange_argmax(bv, bi, engine=engine, group=group)
+    return v, i, results

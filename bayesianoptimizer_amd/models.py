@@ -1,0 +1,146 @@
+"""BoTorch-shaped model and acquisition objects over the gpx engine.
+
+These mirror the reference's operator surface for the hot path so calling code reads like
+``optimization/Bayesian*.py``:
+
+  ExactGP(train_X, train_Y, params, outcome_transform=Standardize)   ≙ SingleTaskGP(train_X, train_Y, ...)
+      .fit()                                                           ≙ building the exact posterior caches
+      .posterior(X).mean / .variance                                   ≙ model.posterior(X) (Bayesian2.py:169-171)
+  LogExpectedImprovement(model, best_f).sweep(X) -> (value, index)     ≙ analytic LogEI + raw-sample argmax
+  ExpectedImprovement / UpperConfidenceBound / PosteriorVariance       ≙ the other analytic scores
+
+Hyperparameters are fixed (no MLL fitting; SURVEY §8f row 1 is the next step).  NOT_PD handling follows the
+reference's jitter-retry policy (optimization/Bayesian6.py:481-488): the factorisation is retried with the
+jitters of ``jitter_schedule`` before the NotPositiveDefiniteError propagates.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import torch
+
+from ._capi import NotPositiveDefiniteError
+from .engine import GPEngine, GPState, KernelParams, botorch_default_lengthscale
+from .transforms import Standardize
+
+
+@dataclass
+class Posterior:
+    mean: torch.Tensor       # (m, T) untransformed
+    variance: torch.Tensor   # (m, T) untransformed (all outputs share the kernel: identical columns scaled)
+
+
+class ExactGP:
+    """Exact GP with up to 8 outputs sharing X and the covariance (one factorisation, T right-hand sides)."""
+
+    def __init__(self, train_X, train_Y, params: Optional[KernelParams] = None,
+                 outcome_transform: Optional[Standardize] = None, engine=None,
+                 jitter_schedule: Sequence[float] = (0.0, 1e-4, 1e-2)):
+        self.engine = engine if engine is not None else GPEngine()
+        dev = getattr(self.engine, "device", None)
+        X = torch.as_tensor(train_X, dtype=torch.float64)
+        Y = torch.as_tensor(train_Y, dtype=torch.float64)
+        if Y.dim() == 1:
+            Y = Y.unsqueeze(-1)
+        if dev is not None:
+            X, Y = X.to(dev), Y.to(dev)
+        self.train_X, self.train_Y = X, Y
+        d = X.shape[1]
+        self.params = params or KernelParams("rbf", botorch_default_lengthscale(d), noise=1e-4)
+        self.outcome_transform = outcome_transform
+        self.jitter_schedule = tuple(jitter_schedule)
+        self.state: Optional[GPState] = None
+        self.jitter_used = None
+
+    @property
+    def num_outputs(self) -> int:
+        return self.train_Y.shape[1]
+
+    @property
+    def lengthscale(self):
+        return self.params.lengthscales(self.train_X.shape[1])
+
+    def fit(self) -> "ExactGP":
+        Y = self.train_Y
+        if self.outcome_transform is not None:
+            Y = self.outcome_transform.fit(Y).transform(Y)
+        last = None
+        for jit in self.jitter_schedule:
+            try:
+                self.state = self.engine.fit(self.train_X, Y, self.params.replace(jitter=jit))
+                self.jitter_used = jit
+                return self
+            except NotPositiveDefiniteError as e:  # reference: retry with larger cholesky_jitter
+                last = e
+        raise last
+
+    def _untransform(self):
+        ot = self.outcome_transform
+        if ot is None:
+            return None, None
+        return [float(v) for v in ot.mean.reshape(-1)], [float(v) for v in ot.std.reshape(-1)]
+
+    def posterior(self, X) -> Posterior:
+        if self.state is None:
+            self.fit()
+        ym, ys = self._untransform()
+        mean, var = self.engine.posterior(self.state, X, ym, ys)
+        # variance of output t = var_std * s_t^2 (the engine returns output 0's scaling)
+        if ys is not None:
+            s = torch.tensor(ys, dtype=torch.float64, device=var.device)
+            var_all = (var / (s[0] * s[0])).unsqueeze(-1) * (s * s)
+            var_all = torch.clamp(var_all, min=1e-12)
+        else:
+            var_all = var.unsqueeze(-1).expand(-1, self.num_outputs).clone()
+        return Posterior(mean=mean, variance=var_all)
+
+
+class _Analytic:
+    kind = "logei"
+
+    def __init__(self, model: ExactGP, best_f: float = 0.0, beta: float = 4.0, output: int = 0,
+                 weights: Optional[Sequence[float]] = None):
+        self.model = model
+        self.best_f = float(best_f)
+        self.beta = float(beta)
+        self.output = output
+        self.weights = weights
+
+    def _objective(self):
+        """(alpha vector, y_mean, y_scale) of the scored output, in the engine's standardized space."""
+        m = self.model
+        if m.state is None:
+            m.fit()
+        ym, ys = m._untransform()
+        if self.weights is not None:
+            raise NotImplementedError("weighted objectives: combine alpha columns before sweeping")
+        alpha = m.state.alpha[:, self.output]
+        if ym is None:
+            return alpha, 0.0, 1.0
+        return alpha, ym[self.output], ys[self.output]
+
+    def sweep(self, X, index_offset: int = 0, return_scores: bool = False):
+        alpha, ym, ys = self._objective()
+        return self.model.engine.acquire(self.model.state, X, self.kind, best_f=self.best_f, beta=self.beta,
+                                         y_mean=ym, y_scale=ys, alpha=alpha, index_offset=index_offset,
+                                         return_scores=return_scores)
+
+    def __call__(self, X) -> torch.Tensor:
+        return self.sweep(X, return_scores=True)[2]
+
+
+class ExpectedImprovement(_Analytic):
+    kind = "ei"
+
+
+class LogExpectedImprovement(_Analytic):
+    kind = "logei"
+
+
+class UpperConfidenceBound(_Analytic):
+    kind = "ucb"
+
+
+class PosteriorVariance(_Analytic):
+    kind = "variance"

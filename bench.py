@@ -1,0 +1,213 @@
+"""Benchmark of the GP-posterior hot path (BASELINE.json metric), one process per GPU.
+
+A step = one posterior update (Gram + blocked Cholesky + L^{-T} + alpha, n=4096, d=8, RBF, fp64) followed by
+a 2^20-candidate analytic logEI sweep with argmax (BASELINE.json configs[1]), then the cross-rank (value,
+index) exchange.  Every rank owns an independent problem (different seed: weak scaling); the
+only collective is an all-gather of one 16-byte record per rank over RCCL.
+
+Prints ONE JSON line on rank 0.  value = candidates scored per second over the whole job
+(= n_gpus * m * steps / max-over-ranks time); the fit-only rate (posterior updates/s) is timed in a second
+loop and reported beside it.  Inputs are resident in HBM before the timed region starts.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from bayesianoptimizer_amd import GPEngine, KernelParams, botorch_default_lengthscale, synthetic  # noqa: E402
+
+METRIC = "GP posterior updates/sec + acq-cands/sec, n=4096 d=8 fp64, 1→8 MI355X"
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix, spec; measured 78.1 TF/s (profiles/r01_probe_f64_rate.log)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=4096)
+    ap.add_argument("--d", type=int, default=8)
+    ap.add_argument("--m", type=int, default=1 << 20)
+    ap.add_argument("--kernel", default="rbf")
+    ap.add_argument("--acq", default="logei")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-sample", type=int, default=8192, help="candidates in the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return dist, rank, world, local
+    torch.cuda.set_device(0)
+    return None, 0, 1, 0
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def pmc_traffic_per_launch():
+    """HBM bytes per trmm launch from the committed rocprofv3 --pmc passes (tools/pmc_traffic.py)."""
+    path = os.path.join(ROOT, "profiles", "trmm_pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(X, y, Xs_np, kind, acq, ls, sample):
+    """Oracle (NumPy/SciPy fp64) on the host cores: one fit + a bounded sample of the same candidate sweep,
+    extrapolated linearly to the full step."""
+    from oracle import gp_oracle as O  # checker / baseline only
+
+    kid = {"rbf": O.RBF, "matern52": O.MATERN52, "scale_linear_matern52": O.SCALE_LINEAR_MATERN52}[kind]
+    aid = {"ei": O.ACQ_EI, "logei": O.ACQ_LOGEI, "ucb": O.ACQ_UCB, "variance": O.ACQ_VARIANCE}[acq]
+    p = O.KernelParams(kid, np.full(X.shape[1], ls), noise=1e-4)
+    t0 = time.perf_counter()
+    st = O.fit(X, y, p)
+    t1 = time.perf_counter()
+    O.acquire_argmax(st, Xs_np[:sample], aid, best_f=float(y.max()), chunk=4096)
+    t2 = time.perf_counter()
+    m = Xs_np.shape[0]
+    step_s = (t1 - t0) + (t2 - t1) * (m / sample)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    return {"value": m / step_s, "unit": "acq-cands/s", "cores": threads, "kind": "port",
+            "sample": f"oracle fit n={X.shape[0]} ({t1 - t0:.2f} s) + {acq} sweep of {sample} of the {m} "
+                      f"candidates ({t2 - t1:.2f} s), extrapolated linearly to one full step ({step_s:.1f} s)"}
+
+
+def main():
+    args = parse()
+    dist, rank, world, local = dist_setup(args)
+    dev = torch.device("cuda", local)
+    seed = args.seed + 1000 * rank
+    X_np, y_np = synthetic.problem(args.n, args.d, seed)
+    Xs_np = synthetic.sobol(args.m, args.d, seed + 1)
+    ls = botorch_default_lengthscale(args.d)
+    params = KernelParams(args.kernel, ls, noise=1e-4)
+    X = torch.tensor(X_np, device=dev)
+    y = torch.tensor(y_np, device=dev)
+    Xs = torch.tensor(Xs_np, device=dev)
+    best_f = float(y_np.max())
+    eng = GPEngine(dev)
+    state = eng.fit(X, y, params)  # allocation + first-touch outside the timed region
+    gather_v = torch.empty((world,), dtype=torch.float64, device=dev)
+    gather_i = torch.empty((world,), dtype=torch.int64, device=dev)
+
+    def step():
+        st = eng.fit(X, y, params, check=False, out=state)
+        bv, bi = eng.acquire(st, Xs, args.acq, best_f=best_f, index_offset=rank * args.m)
+        if dist is not None:
+            dist.all_gather_into_tensor(gather_v, bv)
+            dist.all_gather_into_tensor(gather_i, bi)
+            bv, bi = eng.argmax_combine(gather_v, gather_i)
+        return bv, bi
+
+    for _ in range(args.warmup):
+        step()
+    barrier(dist)
+    eng.timing_reset()
+    eng.timing_enable(["trmm"])
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        bv, bi = step()
+    barrier(dist)
+    elapsed = time.perf_counter() - t0
+    trmm_ms, trmm_launches = eng.timing_query("trmm")
+    eng.timing_disable()
+    if int(state.info.item()) != 0:
+        raise RuntimeError("Cholesky failed inside the benchmark")
+
+    # fit-only loop: posterior updates per second
+    barrier(dist)
+    t2 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.fit(X, y, params, check=False, out=state)
+    barrier(dist)
+    fit_elapsed = time.perf_counter() - t2
+
+    times = torch.tensor([elapsed, fit_elapsed], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(times, op=dist.ReduceOp.MAX)
+    elapsed, fit_elapsed = float(times[0]), float(times[1])
+
+    if rank == 0:
+        m, n = args.m, args.n
+        value = world * m * args.steps / elapsed
+        avg_ms = trmm_ms / max(trmm_launches, 1)
+        cands_per_launch = m * args.steps / max(trmm_launches, 1)
+        flops_per_launch = float(n) * n * cands_per_launch  # n^2 flops per candidate (v = L^-1 k*)
+        achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(X_np, y_np, Xs_np, args.kernel, args.acq, ls, args.cpu_sample)
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "acq-cands/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded U[0,1] X, sin-sum y, scrambled Sobol candidates; fixed hyperparameters)",
+            "config": {
+                "workload": f"BASELINE configs[1]: n={n} d={args.d} {args.kernel.upper()} GP fp64, one posterior "
+                            f"update + {m}-candidate {args.acq} sweep + argmax per step, per GPU",
+                "n": n, "d": args.d, "m": m, "kernel": args.kernel, "acq": args.acq,
+                "parallelism": f"{world} independent problems (one per GPU), RCCL 16-byte argmax all-gather",
+            },
+            "updates_per_s": world * args.steps / fit_elapsed,
+            "fit_ms": 1e3 * fit_elapsed / args.steps,
+            "best": {"value": float(bv.item()), "index": int(bi.item())},
+            "roofline": {
+                "kernel": "trmm_sumsq_kernel (V = L^-1 K*, fp64 MFMA 16x16x4)",
+                "bound": "mfma",
+                "achieved": achieved,
+                "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / FP64_PEAK_TFLOPS,
+                "traffic": pmc_traffic_per_launch(),
+                "avg_launch_ms": avg_ms,
+                "launches": trmm_launches,
+                "flops_per_launch": flops_per_launch,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -317,7 +317,8 @@ def synthetic_problem(n: int, d: int, seed: int, noise_sd: float = 0.01):
     rng = np.random.default_rng(seed)
     X = rng.random((n, d))
     y = np.sin(6.0 * X).sum(axis=1) + noise_sd * rng.standard_normal(n)
-    y = (y - y.mean()) / y.std()
+    sd = y.std()
+    y = (y - y.mean()) / (sd if sd > 0 else 1.0)
     return X, y
 
 
