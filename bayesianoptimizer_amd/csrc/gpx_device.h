@@ -143,29 +143,27 @@ struct MfmaTile {
   }
 
   // Full k loop. smem must hold LDS_DOUBLES doubles.  A/B point at the tile origin (m0 / n0 applied).
+  // One loop body with swapped current/next LDS pointers: the two-branch (even/odd buffer) form made hipcc
+  // rename the accumulators between branches and shuttle them through AGPR moves after dependent MFMAs
+  // (48.7 vs 64.0 TF/s on the n=4096 sweep product, tools/trmm_bench.hip).
   __device__ __forceinline__ void run(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
                                       int64_t ldb, int kbeg, int kend, double* smem) {
     zero();
     if (kend <= kbeg) return;
-    double* sA0 = smem;
-    double* sB0 = smem + BK * PA;
-    double* sA1 = smem + BK * (PA + PB);
-    double* sB1 = sA1 + BK * PA;
+    double* cur = smem;
+    double* nxt = smem + BK * (PA + PB);
     load_regs(A, lda, B, ldb, kbeg);
-    store_lds(sA0, sB0);
+    store_lds(cur, cur + BK * PA);
     __syncthreads();
-    int it = 0;
-    for (int k0 = kbeg; k0 < kend; k0 += BK, ++it) {
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
       const bool more = (k0 + BK) < kend;
       if (more) load_regs(A, lda, B, ldb, k0 + BK);
-      if ((it & 1) == 0) {
-        compute(sA0, sB0);
-        if (more) store_lds(sA1, sB1);
-      } else {
-        compute(sA1, sB1);
-        if (more) store_lds(sA0, sB0);
-      }
+      compute(cur, cur + BK * PA);
+      if (more) store_lds(nxt, nxt + BK * PA);
       __syncthreads();
+      double* t = cur;
+      cur = nxt;
+      nxt = t;
     }
   }
 

@@ -46,6 +46,9 @@ __global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ 
   const double* Bb = W + off2 * ldw + off2 + cb * NB;   // B(k=q,n=c) = W[off2+q][off2+c]
   Tile tile;
   tile.run(Ab, ldl, Bb, ldw, 0, (cb + 1) * NB, smem);
+  // T_p is b1 x b2 with row length b2; every group before the last is full (b2 = b1), so group p starts at
+  // p*b1*b1 and the level's total sum_p b1*b2_p <= b1*(npad-b1) <= npad^2/4 fits the workspace.
+  const int b2 = nb2 * NB;
   double* Tp = T + (int64_t)p * b1 * b1;
 #pragma unroll
   for (int i = 0; i < Tile::WM; ++i)
@@ -53,7 +56,7 @@ __global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ 
     for (int j = 0; j < Tile::WN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        Tp[(int64_t)(rb * NB + Tile::row_of(i, r)) * b1 + cb * NB + Tile::col_of(j)] = tile.acc[i][j][r];
+        Tp[(int64_t)(rb * NB + Tile::row_of(i, r)) * b2 + cb * NB + Tile::col_of(j)] = tile.acc[i][j][r];
 }
 
 // W12 = -W11 T_p
@@ -69,9 +72,10 @@ __global__ void __launch_bounds__(WG) trtri_w_kernel(double* __restrict__ W, int
   const int b1 = h * NB;
   const int64_t off1 = (int64_t)s1 * NB, off2 = (int64_t)s2 * NB;
   const double* Ab = W + (off1 + rb * NB) * ldw + off1;           // A(m=r,k=q) = W[off1+r][off1+q]
-  const double* Bb = T + (int64_t)p * b1 * b1 + cb * NB;          // B(k=q,n=c) = T[q][c]
+  const int b2 = nb2 * NB;
+  const double* Bb = T + (int64_t)p * b1 * b1 + cb * NB;          // B(k=q,n=c) = T[q][c], row length b2
   Tile tile;
-  tile.run(Ab, ldw, Bb, b1, rb * NB, b1, smem);
+  tile.run(Ab, ldw, Bb, b2, rb * NB, b1, smem);
   double* Wo = W + (off1 + rb * NB) * ldw + off2 + cb * NB;
 #pragma unroll
   for (int i = 0; i < Tile::WM; ++i)

@@ -88,26 +88,43 @@ def test_potrf_and_dinv(engine, n):
         np.testing.assert_allclose(D[b] @ blk, np.eye(64), atol=1e-10)
 
 
-@pytest.mark.parametrize("dup_at", [1, 70, 150])
-def test_not_pd_reports_pivot(engine, dup_at):
+@pytest.mark.parametrize("pivot", [0, 1, 70, 150, 511])
+def test_not_pd_reports_pivot(engine, pivot):
+    # SPD matrix whose Schur complement at `pivot` is made exactly -0.5: both LAPACK and the GPU must stop
+    # there (an exactly singular pivot would be +-eps, i.e. rounding-dependent, in any implementation).
+    n = 600
+    rng = np.random.default_rng(pivot)
+    B = rng.standard_normal((n, n)) / np.sqrt(n)
+    A = B @ B.T + np.eye(n)
+    Lp = np.linalg.cholesky(A[:pivot, :pivot]) if pivot else np.zeros((0, 0))
+    schur = A[pivot, pivot] - (np.linalg.solve(Lp, A[:pivot, pivot]) ** 2).sum() if pivot else A[0, 0]
+    A[pivot, pivot] -= schur + 0.5
+    with pytest.raises(O.NotPDError) as e:
+        O.cholesky(A)
+    assert e.value.pivot == pivot
+    npad = engine.padded_n(n)
+    K = torch.eye(npad, dtype=torch.float64, device=DEV)
+    K[:n, :n] = t(A)
+    _, info = engine.potrf(K, n)
+    assert int(info.item()) == pivot + 1
+
+
+def test_fit_raises_not_pd_on_duplicate(engine):
     X, _ = O.synthetic_problem(200, 3, 5)
-    X[dup_at] = X[dup_at - 1]  # exact duplicate, no noise -> singular at pivot dup_at
+    X[1] = X[0]  # exact duplicate at pivot 1, no noise: 1 - 1*1 = 0 exactly
     kp, op = pair("rbf", 3, noise=0.0)
     with pytest.raises(O.NotPDError) as e:
         O.cholesky(O.gram(X, op))
-    K = engine.gram(t(X), kp)
-    _, info = engine.potrf(K, 200)
-    assert int(info.item()) == e.value.pivot + 1
     with pytest.raises(NotPositiveDefiniteError) as e2:
         engine.fit(t(X), t(np.zeros(200)), kp)
-    assert e2.value.pivot == e.value.pivot
+    assert e2.value.pivot == e.value.pivot == 1
 
 
 def test_jitter_retry_on_gpu(engine):
     from bayesianoptimizer_amd.models import ExactGP
 
     X, y = O.synthetic_problem(100, 3, 6)
-    X[10] = X[9]
+    X[1] = X[0]
     gp = ExactGP(X, y, KernelParams("rbf", 0.4, noise=0.0), engine=engine).fit()
     assert gp.jitter_used == 1e-4
 
