@@ -56,6 +56,8 @@ class KernelParamsC(ctypes.Structure):
         ("noise", c_double),
         ("jitter", c_double),
         ("const_mean", c_double),
+        ("cov_fp32", c_int32),
+        ("reserved", c_int32),
     ]
 
 

@@ -18,6 +18,17 @@ __device__ __forceinline__ double cov_from_r2(int kind, double outputscale, doub
   return outputscale * (lin + m);
 }
 
+// fp32 evaluation (gpx_kernel_params.cov_fp32, BASELINE configs[4]): r2 accumulated in fp32 from fp32-rounded
+// scaled inputs, exp / sqrt / Matern polynomial in fp32, widened to fp64 before the outputscale and linear part.
+__device__ __forceinline__ double cov_from_r2_f32(int kind, double outputscale, float r2, double lin) {
+  if (kind == GPX_KERNEL_RBF) return outputscale * (double)expf(-0.5f * r2);
+  const float r = sqrtf(r2);
+  const float s5r = 2.2360679774997897f * r;
+  const float m = (1.0f + s5r + (5.0f / 3.0f) * r2) * expf(-s5r);
+  if (kind == GPX_KERNEL_MATERN52) return outputscale * (double)m;
+  return outputscale * (lin + (double)m);
+}
+
 // Linear index t over the lower triangle of an m x m block grid (row-major order of (i, j), j <= i)
 // -> (i, j).
 __device__ __forceinline__ void tri_decode(int t, int& i, int& j) {

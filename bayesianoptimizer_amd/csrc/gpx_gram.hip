@@ -10,7 +10,7 @@
 
 namespace gpx {
 
-template <int DMAX>
+template <int DMAX, bool F32>
 __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, int nblk, const double* __restrict__ X,
                                                   int64_t ldx, double* __restrict__ K, int64_t ldk) {
   __shared__ double si[NB][DMAX + 1], sj[NB][DMAX + 1];    // scaled x / l
@@ -47,16 +47,33 @@ __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, in
     const int gi = i0 + r;
     double v;
     if (gi < n && gj < n) {
-      double r2 = 0.0, lv = 0.0;
+      double lv = 0.0;
+      if (lin) {
 #pragma unroll
-      for (int k = 0; k < DMAX; ++k) {
-        if (k < d) {
-          const double df = si[r][k] - xc[k];
-          r2 += df * df;
-          if (lin) lv += ri[r][k] * rc[k];
-        }
+        for (int k = 0; k < DMAX; ++k)
+          if (k < d) lv += ri[r][k] * rc[k];
       }
-      v = cov_from_r2(p.kind, p.outputscale, r2, lv);
+      if (F32) {
+        float r2 = 0.0f;
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) {
+          if (k < d) {
+            const float df = (float)si[r][k] - (float)xc[k];
+            r2 += df * df;
+          }
+        }
+        v = cov_from_r2_f32(p.kind, p.outputscale, r2, lv);
+      } else {
+        double r2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) {
+          if (k < d) {
+            const double df = si[r][k] - xc[k];
+            r2 += df * df;
+          }
+        }
+        v = cov_from_r2(p.kind, p.outputscale, r2, lv);
+      }
       if (gi == gj) v += diag_add;
     } else {
       v = (gi == gj) ? 1.0 : 0.0;  // identity padding
@@ -70,14 +87,18 @@ hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, 
   LaunchTimer tm(c, GPX_TIMER_GRAM);
   const int nblk = npad / NB;
   const int tiles = nblk * (nblk + 1) / 2;
+#define GPX_GRAM(D)                                                                       \
+  (p.cov_fp32 ? gram_kernel<D, true><<<tiles, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk) \
+              : gram_kernel<D, false><<<tiles, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk))
   if (p.d <= 4)
-    gram_kernel<4><<<tiles, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk);
+    GPX_GRAM(4);
   else if (p.d <= 8)
-    gram_kernel<8><<<tiles, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk);
+    GPX_GRAM(8);
   else if (p.d <= 16)
-    gram_kernel<16><<<tiles, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk);
+    GPX_GRAM(16);
   else
-    gram_kernel<32><<<tiles, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk);
+    GPX_GRAM(32);
+#undef GPX_GRAM
   return hipGetLastError();
 }
 

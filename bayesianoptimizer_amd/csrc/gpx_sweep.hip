@@ -70,7 +70,7 @@ __device__ __forceinline__ void load_point(const gpx_kernel_params& p, const dou
 }
 
 // ---- 1. K* and partial means ---------------------------------------------------------------------------
-template <int DMAX>
+template <int DMAX, bool F32>
 __global__ void __launch_bounds__(WG) kstar_kernel(gpx_kernel_params p, int n, const double* __restrict__ X,
                                                    int64_t ldx, const double* __restrict__ alpha, int nrhs,
                                                    const double* __restrict__ Xs, int64_t ldxs, int64_t m_chunk,
@@ -103,16 +103,33 @@ __global__ void __launch_bounds__(WG) kstar_kernel(gpx_kernel_params p, int n, c
   for (int j = 0; j < NB; ++j) {
     double kv = 0.0;
     if (j0 + j < n) {
-      double r2 = 0.0, lv = 0.0;
+      double lv = 0.0;
+      if (lin) {
 #pragma unroll
-      for (int k = 0; k < DMAX; ++k) {
-        if (k < d) {
-          const double df = sx[j][k] - xs[k];
-          r2 += df * df;
-          if (lin) lv += sr[j][k] * xr[k];
-        }
+        for (int k = 0; k < DMAX; ++k)
+          if (k < d) lv += sr[j][k] * xr[k];
       }
-      kv = cov_from_r2(p.kind, p.outputscale, r2, lv);
+      if (F32) {
+        float r2 = 0.0f;
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) {
+          if (k < d) {
+            const float df = (float)sx[j][k] - (float)xs[k];
+            r2 += df * df;
+          }
+        }
+        kv = cov_from_r2_f32(p.kind, p.outputscale, r2, lv);
+      } else {
+        double r2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) {
+          if (k < d) {
+            const double df = sx[j][k] - xs[k];
+            r2 += df * df;
+          }
+        }
+        kv = cov_from_r2(p.kind, p.outputscale, r2, lv);
+      }
     }
     kstar[(int64_t)(j0 + j) * C + c] = kv;
 #pragma unroll
@@ -312,14 +329,20 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
   {
     LaunchTimer tm(c, GPX_TIMER_KSTAR);
     dim3 g(ncb, nJB);
+#define GPX_KSTAR(D)                                                                                               \
+  (p.cov_fp32 ? kstar_kernel<D, true><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk, C,    \
+                                                               b.kstar, b.mu_part)                               \
+              : kstar_kernel<D, false><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk, C,   \
+                                                                b.kstar, b.mu_part))
     if (p.d <= 4)
-      kstar_kernel<4><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk, C, b.kstar, b.mu_part);
+      GPX_KSTAR(4);
     else if (p.d <= 8)
-      kstar_kernel<8><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk, C, b.kstar, b.mu_part);
+      GPX_KSTAR(8);
     else if (p.d <= 16)
-      kstar_kernel<16><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk, C, b.kstar, b.mu_part);
+      GPX_KSTAR(16);
     else
-      kstar_kernel<32><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk, C, b.kstar, b.mu_part);
+      GPX_KSTAR(32);
+#undef GPX_KSTAR
   }
   {
     LaunchTimer tm(c, GPX_TIMER_TRMM);

@@ -49,6 +49,7 @@ class KernelParams:
     jitter: float = 0.0
     const_mean: float = 0.0
     linear_variance: Union[float, Sequence[float]] = 1.0
+    cov_fp32: bool = False  # fp32 covariance evaluation, fp64 factorisation (BASELINE configs[4])
 
     @property
     def kind_id(self) -> int:
@@ -87,6 +88,7 @@ class KernelParams:
         c.noise = float(self.noise)
         c.jitter = float(self.jitter)
         c.const_mean = float(self.const_mean)
+        c.cov_fp32 = 1 if self.cov_fp32 else 0
         return c
 
     def replace(self, **kw) -> "KernelParams":

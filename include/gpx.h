@@ -77,6 +77,10 @@ typedef struct {
   double noise;                          /* GaussianLikelihood noise sigma^2 */
   double jitter;                         /* extra diagonal (gpytorch.settings.cholesky_jitter) */
   double const_mean;                     /* ConstantMean */
+  int32_t cov_fp32;                      /* 1: evaluate distances / exp / Matérn polynomial in fp32 (BASELINE
+                                            configs[4] mixed-precision build), widen to fp64 before the fp64
+                                            factorisation and sweep; 0: fp64 throughout */
+  int32_t reserved;
 } gpx_kernel_params;
 
 typedef struct {

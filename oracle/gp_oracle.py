@@ -67,6 +67,7 @@ class KernelParams:
     const_mean: float = 0.0
     linear_variance: Optional[np.ndarray] = None
     jitter: float = 0.0
+    cov_fp32: bool = False  # BASELINE configs[4]: covariance evaluated in fp32, widened before factorisation
 
     def __post_init__(self):
         self.lengthscale = np.asarray(self.lengthscale, dtype=np.float64).reshape(-1)
@@ -106,6 +107,8 @@ def kernel_matrix(X1: np.ndarray, X2: np.ndarray, p: KernelParams) -> np.ndarray
     """k(X1, X2) without noise.  Formulas per GPyTorch RBFKernel/MaternKernel/LinearKernel/ScaleKernel."""
     X1 = np.asarray(X1, dtype=np.float64)
     X2 = np.asarray(X2, dtype=np.float64)
+    if p.cov_fp32:
+        return _kernel_matrix_f32(X1, X2, p)
     r2 = _sqdist_scaled(X1, X2, p.lengthscale)
     if p.kind == RBF:
         return p.outputscale * np.exp(-0.5 * r2)
@@ -118,6 +121,26 @@ def kernel_matrix(X1: np.ndarray, X2: np.ndarray, p: KernelParams) -> np.ndarray
         lin = (X1 * p.linear_variance) @ X2.T
         return p.outputscale * (lin + matern)
     raise ValueError(f"unknown kernel kind {p.kind}")
+
+
+def _kernel_matrix_f32(X1, X2, p: KernelParams) -> np.ndarray:
+    """fp32 evaluation: scaled inputs rounded to fp32, squared distance summed in fp32 (k = 0..d-1), exp and the
+    Matern polynomial in fp32, widened to fp64 before the outputscale and the (fp64) linear part."""
+    A = (X1 / p.lengthscale).astype(np.float32)
+    B = (X2 / p.lengthscale).astype(np.float32)
+    r2 = np.zeros((A.shape[0], B.shape[0]), dtype=np.float32)
+    for k in range(A.shape[1]):
+        diff = A[:, k:k + 1] - B[None, :, k]
+        r2 += diff * diff
+    if p.kind == RBF:
+        return p.outputscale * np.exp(np.float32(-0.5) * r2).astype(np.float64)
+    r = np.sqrt(r2)
+    s5r = np.float32(math.sqrt(5.0)) * r
+    m = ((np.float32(1.0) + s5r + np.float32(5.0 / 3.0) * r2) * np.exp(-s5r)).astype(np.float64)
+    if p.kind == MATERN52:
+        return p.outputscale * m
+    lin = (X1 * p.linear_variance) @ X2.T
+    return p.outputscale * (lin + m)
 
 
 def kernel_diag(X: np.ndarray, p: KernelParams) -> np.ndarray:

@@ -41,8 +41,9 @@ def test_version_and_padding(lib):
 
 
 def test_struct_layout_matches_header():
-    # gpx_kernel_params: 2 int32 + 2*32 doubles + 4 doubles
-    assert ctypes.sizeof(_capi.KernelParamsC) == 8 + 2 * 32 * 8 + 4 * 8
+    # gpx_kernel_params: 2 int32 + 2*32 doubles + 4 doubles + 2 int32
+    assert ctypes.sizeof(_capi.KernelParamsC) == 8 + 2 * 32 * 8 + 4 * 8 + 8
+    assert _capi.KernelParamsC.cov_fp32.offset == 8 + 2 * 32 * 8 + 4 * 8
     assert _capi.KernelParamsC.lengthscale.offset == 8
     assert _capi.KernelParamsC.outputscale.offset == 8 + 2 * 32 * 8
     assert ctypes.sizeof(_capi.AcqParamsC) == 8 + 4 * 8
