@@ -133,23 +133,37 @@ struct MfmaTile {
     }
   }
 
-  __device__ __forceinline__ void compute(const double* sA, const double* sB) {
+  __device__ __forceinline__ void frag(const double* sA, const double* sB, int ks, double* a, double* b) {
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     const int wm0 = (w >> 1) * (TM / 2);
     const int wn0 = (w & 1) * (TN / 2);
     const int kr = lane >> 4, cl = lane & 15;
 #pragma unroll
-    for (int ks = 0; ks < BK; ks += 4) {
-      double a[WM], b[WN];
+    for (int i = 0; i < WM; ++i) a[i] = sA[(ks + kr) * PA + wm0 + 16 * i + cl];
 #pragma unroll
-      for (int i = 0; i < WM; ++i) a[i] = sA[(ks + kr) * PA + wm0 + 16 * i + cl];
+    for (int j = 0; j < WN; ++j) b[j] = sB[(ks + kr) * PB + wn0 + 16 * j + cl];
+  }
+
+  __device__ __forceinline__ void mm(const double* a, const double* b) {
 #pragma unroll
-      for (int j = 0; j < WN; ++j) b[j] = sB[(ks + kr) * PB + wn0 + 16 * j + cl];
+    for (int i = 0; i < WM; ++i)
 #pragma unroll
-      for (int i = 0; i < WM; ++i)
+      for (int j = 0; j < WN; ++j) acc[i][j] = mfma16x16x4(a[i], b[j], acc[i][j]);
+  }
+
+  // Fragments are register double-buffered: the next k-substep's ds_reads are issued before the current
+  // substep's MFMAs (+2-4 % on the sweep product, tools/trmm_bench.hip v5).
+  __device__ __forceinline__ void compute(const double* sA, const double* sB) {
+    static_assert(BK % 8 == 0, "BK must be a multiple of 8");
+    double a0[WM], b0[WN], a1[WM], b1[WN];
+    frag(sA, sB, 0, a0, b0);
 #pragma unroll
-        for (int j = 0; j < WN; ++j) acc[i][j] = mfma16x16x4(a[i], b[j], acc[i][j]);
+    for (int ks = 0; ks < BK; ks += 8) {
+      frag(sA, sB, ks + 4, a1, b1);
+      mm(a0, b0);
+      if (ks + 8 < BK) frag(sA, sB, ks + 8, a0, b0);
+      mm(a1, b1);
     }
   }
 

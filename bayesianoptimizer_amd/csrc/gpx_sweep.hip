@@ -16,6 +16,7 @@
 // launch_argmax_final reduces the records of the whole sweep in one workgroup.
 #include "gpx_internal.h"
 #include "gpx_device.h"
+#include <cstdlib>
 
 namespace gpx {
 
@@ -48,6 +49,22 @@ __device__ __forceinline__ double acq_score(int kind, double mu, double var, dou
   if (kind == GPX_ACQ_LOGEI) return log_ei_helper_d((mu - best_f) / sigma) + log(sigma);
   if (kind == GPX_ACQ_UCB) return mu + sqrt(beta) * sigma;
   return var;
+}
+
+// Sum of `cnt` partials spaced `stride` apart, in a fixed order: 8 independent loads in flight per group
+// (a plain loop over a runtime count waited for every load before the next: 32 serial round trips).
+__device__ __forceinline__ double sum_partials(const double* __restrict__ p, int cnt, int64_t stride) {
+  double s = 0.0;
+  int i = 0;
+  for (; i + 8 <= cnt; i += 8) {
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = p[(int64_t)(i + q) * stride];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += v[q];
+  }
+  for (; i < cnt; ++i) s += p[(int64_t)i * stride];
+  return s;
 }
 
 // (value, index) order: larger value wins, equal values -> lower index; NaN already mapped to -inf.
@@ -215,21 +232,18 @@ __global__ void __launch_bounds__(WG) finalize_kernel(FinalizeArgs fa, int mode,
       }
       kd = p.outputscale * (lv + 1.0);
     }
-    double ss = 0.0;
-    for (int I = 0; I < nI; ++I) ss += ss_part[(int64_t)I * C + c];
+    const double ss = sum_partials(ss_part + c, nI, C);
     double var = fmax(kd - ss, 1e-10);  // gpytorch min_variance (float64) [upstream]
     if (mode == 0) {
       for (int q = 0; q < nrhs; ++q) {
-        double mu = 0.0;
-        for (int jb = 0; jb < nJB; ++jb) mu += mu_part[((int64_t)jb * nrhs + q) * C + c];
+        double mu = sum_partials(mu_part + (int64_t)q * C + c, nJB, (int64_t)nrhs * C);
         mu += p.const_mean;
         mean_out[c * ldmean + q] = fa.y_mean[q] + fa.y_scale[q] * mu;
       }
       var_out[c] = fmax(var * (fa.y_scale[0] * fa.y_scale[0]), 1e-12);  // BoTorch min_var [upstream]
       return;
     }
-    double mu = 0.0;
-    for (int jb = 0; jb < nJB; ++jb) mu += mu_part[(int64_t)jb * C + c];
+    double mu = sum_partials(mu_part + c, nJB, C);
     mu = fa.y_mean[0] + fa.y_scale[0] * (mu + p.const_mean);
     var = fmax(var * (fa.y_scale[0] * fa.y_scale[0]), 1e-12);
     score = acq_score(fa.acq_kind, mu, var, fa.best_f, fa.beta);
@@ -296,8 +310,14 @@ __global__ void __launch_bounds__(WG) argmax_final_kernel(const double* __restri
 // ---- host side -------------------------------------------------------------------------------------------
 int64_t sweep_chunk_size(int64_t npad, int64_t m) {
   // K* chunk capped at ~256 MiB (it is re-read (I+1) times by trmm_sumsq; keeping it near the 256 MiB
-  // Infinity Cache helps), at most 16384 candidates, multiple of 256.
-  int64_t cap = ((int64_t)1 << 25) / npad;  // doubles per row budget: 2^28 bytes / 8 / npad
+  // Infinity Cache helps), at most 16384 candidates, multiple of 256.  GPX_SWEEP_CHUNK_MB overrides the byte
+  // budget (experiments).
+  static const int64_t budget_mb = [] {
+    const char* e = getenv("GPX_SWEEP_CHUNK_MB");
+    const long v = e ? atol(e) : 0;
+    return (int64_t)(v > 0 ? v : 256);
+  }();
+  int64_t cap = budget_mb * ((int64_t)1 << 20) / 8 / npad;
   cap = (cap / 256) * 256;
   if (cap < 256) cap = 256;
   if (cap > 16384) cap = 16384;

@@ -38,6 +38,291 @@ struct Tile2 : public MfmaTile<TM, TN, BK, AK, BKM> {
   }
 };
 
+// Generalised tile: WMW x WNW waves (64 x 64 each), NT threads, single-body loop.
+template <int WMW, int WNW, int BK>
+struct Tile3 {
+  static constexpr int NT = 64 * WMW * WNW;
+  static constexpr int TM = 64 * WMW, TN = 64 * WNW;
+  static constexpr int WM = 4, WN = 4;
+  static constexpr int PA = TM + 16, PB = TN + 16;
+  static constexpr int LDS_DOUBLES = 2 * BK * (PA + PB);
+  static constexpr int A_LOADS = TM * BK / (2 * NT), B_LOADS = TN * BK / (2 * NT);
+  d4 acc[4][4];
+  double2 ra[A_LOADS], rb[B_LOADS];
+  __device__ __forceinline__ void load_regs(const double* A, int64_t lda, const double* B, int64_t ldb, int k0) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < A_LOADS; ++q) { int e = (t + q * NT) * 2; int kk = e / TM, mm = e % TM;
+      ra[q] = *reinterpret_cast<const double2*>(A + (int64_t)(k0 + kk) * lda + mm); }
+#pragma unroll
+    for (int q = 0; q < B_LOADS; ++q) { int e = (t + q * NT) * 2; int kk = e / TN, nn = e % TN;
+      rb[q] = *reinterpret_cast<const double2*>(B + (int64_t)(k0 + kk) * ldb + nn); }
+  }
+  __device__ __forceinline__ void store_lds(double* sA, double* sB) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < A_LOADS; ++q) { int e = (t + q * NT) * 2; int kk = e / TM, mm = e % TM;
+      *reinterpret_cast<double2*>(sA + kk * PA + mm) = ra[q]; }
+#pragma unroll
+    for (int q = 0; q < B_LOADS; ++q) { int e = (t + q * NT) * 2; int kk = e / TN, nn = e % TN;
+      *reinterpret_cast<double2*>(sB + kk * PB + nn) = rb[q]; }
+  }
+  __device__ __forceinline__ void compute(const double* sA, const double* sB) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wm0 = (w / WNW) * 64, wn0 = (w % WNW) * 64;
+    const int kr = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int ks = 0; ks < BK; ks += 4) {
+      double a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = sA[(ks + kr) * PA + wm0 + 16 * i + cl];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = sB[(ks + kr) * PB + wn0 + 16 * j + cl];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x4(a[i], b[j], acc[i][j]);
+    }
+  }
+  __device__ __forceinline__ void run(const double* A, int64_t lda, const double* B, int64_t ldb, int kbeg, int kend,
+                                      double* smem) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (d4){0, 0, 0, 0};
+    double* cur = smem;
+    double* nxt = smem + BK * (PA + PB);
+    load_regs(A, lda, B, ldb, kbeg);
+    store_lds(cur, cur + BK * PA);
+    __syncthreads();
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+      const bool more = (k0 + BK) < kend;
+      if (more) load_regs(A, lda, B, ldb, k0 + BK);
+      compute(cur, cur + BK * PA);
+      if (more) store_lds(nxt, nxt + BK * PA);
+      __syncthreads();
+      double* tt = cur; cur = nxt; nxt = tt;
+    }
+  }
+};
+
+// Tile5: Tile2 with explicit register double-buffering of the MFMA fragments (next k-substep's ds_reads
+// issued before the current substep's 16 MFMAs).
+template <int BK>
+struct Tile5 : public MfmaTile<T128, T128, BK, true, true> {
+  using B_ = MfmaTile<T128, T128, BK, true, true>;
+  __device__ __forceinline__ void frag(const double* sA, const double* sB, int ks, double* a, double* b) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int wm0 = (w >> 1) * 64, wn0 = (w & 1) * 64, kr = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = sA[(ks + kr) * B_::PA + wm0 + 16 * i + cl];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = sB[(ks + kr) * B_::PB + wn0 + 16 * j + cl];
+  }
+  __device__ __forceinline__ void mm(const double* a, const double* b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) this->acc[i][j] = mfma16x16x4(a[i], b[j], this->acc[i][j]);
+  }
+  __device__ __forceinline__ void compute2(const double* sA, const double* sB) {
+    double a0[4], b0[4], a1[4], b1[4];
+    frag(sA, sB, 0, a0, b0);
+#pragma unroll
+    for (int ks = 0; ks < BK; ks += 8) {
+      frag(sA, sB, ks + 4, a1, b1);
+      mm(a0, b0);
+      if (ks + 8 < BK) frag(sA, sB, ks + 8, a0, b0);
+      mm(a1, b1);
+    }
+  }
+  __device__ __forceinline__ void run(const double* A, int64_t lda, const double* B, int64_t ldb, int kbeg, int kend,
+                                      double* smem) {
+    this->zero();
+    double* cur = smem;
+    double* nxt = smem + BK * (B_::PA + B_::PB);
+    this->load_regs(A, lda, B, ldb, kbeg);
+    this->store_lds(cur, cur + BK * B_::PA);
+    __syncthreads();
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+      const bool more = (k0 + BK) < kend;
+      if (more) this->load_regs(A, lda, B, ldb, k0 + BK);
+      compute2(cur, cur + BK * B_::PA);
+      if (more) this->store_lds(nxt, nxt + BK * B_::PA);
+      __syncthreads();
+      double* tt = cur; cur = nxt; nxt = tt;
+    }
+  }
+};
+// V6: no LDS, no barriers: every wave streams its own A/B fragments straight from L2 into registers,
+// prefetching PF k-substeps ahead.
+template <int PF>
+__global__ void __launch_bounds__(WG) v6(const double* W, int64_t ldw, const double* K, int64_t C, int nI, double* ss) {
+  __shared__ double red[128];
+  const int I = nI - 1 - blockIdx.y, cb = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wm0 = (w >> 1) * 64, wn0 = (w & 1) * 64, kr = lane >> 4, cl = lane & 15;
+  const double* A = W + (int64_t)I * T128 + wm0 + cl;          // A(m,k) = W[k][I*128 + m]
+  const double* B = K + (int64_t)cb * T128 + wn0 + cl;         // B(k,n) = K[k][cb*128 + n]
+  d4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (d4){0, 0, 0, 0};
+  const int kend = (I + 1) * T128;
+  double a[PF][4], b[PF][4];
+#pragma unroll
+  for (int p = 0; p < PF; ++p) {
+    const int k = 4 * p + kr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { a[p][i] = A[(int64_t)k * ldw + 16 * i]; b[p][i] = B[(int64_t)k * C + 16 * i]; }
+  }
+  for (int k0 = 0; k0 < kend; k0 += 4 * PF) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      double ca[4], cbv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { ca[i] = a[p][i]; cbv[i] = b[p][i]; }
+      const int kn = k0 + 4 * (p + PF) + kr;
+      if (kn < kend) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { a[p][i] = A[(int64_t)kn * ldw + 16 * i]; b[p][i] = B[(int64_t)kn * C + 16 * i]; }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x4(ca[i], cbv[j], acc[i][j]);
+    }
+  }
+  double s[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double v = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v += acc[i][j][r] * acc[i][j][r];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    s[j] = v;
+  }
+  if ((w >> 1) == 1 && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[wn0 + 16 * j + lane] = s[j];
+  }
+  __syncthreads();
+  if ((w >> 1) == 0 && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) ss[(int64_t)I * C + (int64_t)cb * T128 + wn0 + 16 * j + lane] = s[j] + red[wn0 + 16 * j + lane];
+  }
+}
+
+template <class Tile>
+__device__ __forceinline__ void sumsq_epilogue(Tile& tile, double* smem, double* out);
+template <int BK, bool PAIRS>
+__global__ void __launch_bounds__(WG) v5(const double* W, int64_t ldw, const double* K, int64_t C, int nI, double* ss) {
+  using Tile = Tile5<BK>;
+  __shared__ __attribute__((aligned(16))) double smem[Tile::LDS_DOUBLES];
+  if (!PAIRS) {
+    const int I = nI - 1 - blockIdx.y, cb = blockIdx.x;
+    Tile tile;
+    tile.run(W + (int64_t)I * T128, ldw, K + (int64_t)cb * T128, C, 0, (I + 1) * T128, smem);
+    sumsq_epilogue(tile, smem, ss + (int64_t)I * C + (int64_t)cb * T128);
+    return;
+  }
+  const int npair = nI / 2;
+  const int b = blockIdx.x, x = b & 7, l = b >> 3;
+  const int cb = 8 * (l / npair) + x, p = l % npair;
+  for (int h = 0; h < 2; ++h) {
+    const int I = h == 0 ? (nI - 1 - p) : p;
+    Tile tile;
+    tile.run(W + (int64_t)I * T128, ldw, K + (int64_t)cb * T128, C, 0, (I + 1) * T128, smem);
+    sumsq_epilogue(tile, smem, ss + (int64_t)I * C + (int64_t)cb * T128);
+  }
+}
+
+// glds variant: operands go global -> LDS directly (global_load_lds_dwordx4, one 1 KiB row per wave
+// instruction), two LDS stages, no VGPR staging.
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void glb_void;
+template <int BK>
+struct Tile4 : public MfmaTile<T128, T128, BK, true, true> {
+  using B_ = MfmaTile<T128, T128, BK, true, true>;
+  __device__ __forceinline__ void issue(const double* A, int64_t lda, const double* B, int64_t ldb, int k0, double* st) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double* sA = st;
+    double* sB = st + BK * B_::PA;
+#pragma unroll
+    for (int q = 0; q < BK / 4; ++q) {
+      const int kk = w * (BK / 4) + q;
+      __builtin_amdgcn_global_load_lds((glb_void*)(A + (int64_t)(k0 + kk) * lda + 2 * lane), (lds_void*)(sA + kk * B_::PA), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_void*)(B + (int64_t)(k0 + kk) * ldb + 2 * lane), (lds_void*)(sB + kk * B_::PB), 16, 0, 0);
+    }
+  }
+  __device__ __forceinline__ void run(const double* A, int64_t lda, const double* B, int64_t ldb, int kbeg, int kend,
+                                      double* smem) {
+    this->zero();
+    double* cur = smem;
+    double* nxt = smem + BK * (B_::PA + B_::PB);
+    issue(A, lda, B, ldb, kbeg, cur);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+      const bool more = (k0 + BK) < kend;
+      if (more) issue(A, lda, B, ldb, k0 + BK, nxt);
+      this->compute(cur, cur + BK * B_::PA);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      double* tt = cur; cur = nxt; nxt = tt;
+    }
+  }
+};
+template <int BK>
+__global__ void __launch_bounds__(WG) v4(const double* W, int64_t ldw, const double* K, int64_t C, int nI, double* ss) {
+  using Tile = Tile4<BK>;
+  __shared__ __attribute__((aligned(16))) double smem[Tile::LDS_DOUBLES];
+  const int I = nI - 1 - blockIdx.y, cb = blockIdx.x;
+  Tile tile;
+  tile.run(W + (int64_t)I * T128, ldw, K + (int64_t)cb * T128, C, 0, (I + 1) * T128, smem);
+  sumsq_epilogue(tile, smem, ss + (int64_t)I * C + (int64_t)cb * T128);
+}
+
+// 8-wave variant: 256 (rows) x 128 (candidates) tile, per-wave column sums reduced through LDS.
+template <int BK>
+__global__ void __launch_bounds__(512) v3(const double* W, int64_t ldw, const double* K, int64_t C, int nI2, double* ss) {
+  using T = Tile3<4, 2, BK>;
+  __shared__ __attribute__((aligned(16))) double smem[T::LDS_DOUBLES];
+  const int I2 = nI2 - 1 - blockIdx.y, cb = blockIdx.x;  // 256-row tile index, heavy first
+  T tile;
+  tile.run(W + (int64_t)I2 * 256, ldw, K + (int64_t)cb * 128, C, 0, (I2 + 1) * 256, smem);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wr = w / 2, wc = w % 2;  // wave row (0..3) -> 64-row slice, wave col
+  double s[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double v = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v += tile.acc[i][j][r] * tile.acc[i][j][r];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    s[j] = v;
+  }
+  // each 128-row half of the 256 tile maps to one 128-row ss slot: waves wr=0,1 -> slot 2*I2, wr=2,3 -> 2*I2+1
+  double* red = smem;  // [4 wave rows][128 cols]
+  __syncthreads();
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[wr * 128 + wc * 64 + 16 * j + lane] = s[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < 256) {
+    const int half = threadIdx.x >> 7, col = threadIdx.x & 127;
+    ss[(int64_t)(2 * I2 + half) * C + (int64_t)cb * 128 + col] = red[(2 * half) * 128 + col] + red[(2 * half + 1) * 128 + col];
+  }
+}
+
 template <class Tile>
 __device__ __forceinline__ void sumsq_epilogue(Tile& tile, double* smem, double* out) {
   double s[Tile::WN];
@@ -76,15 +361,20 @@ __global__ void __launch_bounds__(WG) v0(const double* W, int64_t ldw, const dou
   sumsq_epilogue(tile, smem, ss + (int64_t)I * C + (int64_t)cb * T128);
 }
 
-// V2: single-body tile core
+// V2: single-body tile core (+ per-WG clock stamps: memtime = shader clock, memrealtime = 100 MHz)
+__device__ unsigned long long g_clk[2 * 65536];
 template <int BK, int MINW>
 __global__ void __launch_bounds__(WG, MINW) v2(const double* W, int64_t ldw, const double* K, int64_t C, int nI, double* ss) {
   using Tile = Tile2<T128, T128, BK, true, true>;
   __shared__ __attribute__((aligned(16))) double smem[Tile::LDS_DOUBLES];
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   const int I = nI - 1 - blockIdx.y, cb = blockIdx.x;
   Tile tile;
   tile.run(W + (int64_t)I * T128, ldw, K + (int64_t)cb * T128, C, 0, (I + 1) * T128, smem);
   sumsq_epilogue(tile, smem, ss + (int64_t)I * C + (int64_t)cb * T128);
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  const int b = blockIdx.y * gridDim.x + blockIdx.x;
+  if (threadIdx.x == 0 && b < 65536) { g_clk[2 * b] = t1 - t0; g_clk[2 * b + 1] = r1 - r0; }
 }
 
 // V1: equal-work pairs (I, nI-1-I) per workgroup; optional XCD-aware remap so the 16 pair-WGs of a candidate
@@ -142,13 +432,13 @@ int main(int argc, char** argv) {
     auto run = [&](int which) {
       const int ncb = C / T128;
       if (which == 0) v0<16><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss0);
-      if (which == 1) v1<16, false><<<ncb * nI / 2, WG>>>(W, n, K, C, nI, ss1);
-      if (which == 2) v1<16, true><<<ncb * nI / 2, WG>>>(W, n, K, C, nI, ss1);
-      if (which == 3) v2<16, 1><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
+      if (which == 1) v5<16, false><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
+      if (which == 2) v6<2><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
+      if (which == 3) v6<4><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
       if (which == 4) v2<16, 2><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
-      if (which == 5) v2<32, 1><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
+      if (which == 5) v4<16><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
     };
-    const char* names[] = {"v0 heavy-first BK16", "v1 pairs BK16", "v1 pairs+xcd BK16", "v2 single BK16", "v2 single BK16 lb2", "v2 single BK32"};
+    const char* names[] = {"v0 heavy-first BK16", "v5 fragdb", "v6 noLDS pf2", "v6 noLDS pf4", "v2 single BK16 lb2", "v4 glds BK16"};
     const int NV = 6;
     std::vector<std::vector<float>> t(NV);
     for (int w = 0; w < NV; ++w) run(w);
@@ -176,6 +466,16 @@ int main(int argc, char** argv) {
       printf("C=%d %-22s median %.3f ms min %.3f ms -> %.2f TF/s\n", C, names[w], t[w][t[w].size() / 2], t[w][0],
              flops / (t[w][t[w].size() / 2] * 1e-3) / 1e12);
     }
+  }
+  {  // sustained clock of v2 after ~1 s of back-to-back launches
+    for (int i = 0; i < 300; ++i) v2<16, 1><<<dim3(64, nI), WG>>>(W, n, K, 8192, nI, ss1);
+    CK(hipDeviceSynchronize());
+    std::vector<unsigned long long> h(2 * 64 * nI);
+    CK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_clk), h.size() * 8));
+    std::vector<double> ghz;
+    for (int b = 0; b < 64 * nI; ++b) if (h[2*b+1] > 1000) ghz.push_back((double)h[2*b] / (double)h[2*b+1] * 0.1);
+    std::sort(ghz.begin(), ghz.end());
+    printf("v2 sustained in-kernel clock: median %.3f GHz (p10 %.3f, p90 %.3f)\n", ghz[ghz.size()/2], ghz[ghz.size()/10], ghz[9*ghz.size()/10]);
   }
   printf("TRMM BENCH DONE\n");
   return 0;
