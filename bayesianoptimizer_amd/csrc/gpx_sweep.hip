@@ -161,11 +161,23 @@ constexpr int TT = 128;  // trmm tile (rows of V x candidates)
 using TrmmTile = MfmaTile<TT, TT, 16, true, true>;
 
 __global__ void __launch_bounds__(WG) trmm_sumsq_kernel(const double* __restrict__ W, int64_t ldw,
-                                                        const double* __restrict__ kstar, int64_t C, int nI,
+                                                        const double* __restrict__ kstar, int64_t C, int nI, int ncb,
                                                         double* __restrict__ ss_part) {
   __shared__ __attribute__((aligned(16))) double smem[TrmmTile::LDS_DOUBLES];
-  const int I = nI - 1 - blockIdx.y;  // heaviest row tiles are dispatched first
-  const int cb = blockIdx.x;
+  // Heaviest row tiles first.  XCD-aware when the candidate tiles split evenly over the 8 XCDs: workgroups
+  // b, b+8, ... share an XCD (dispatch is round-robin; speed only, never correctness), so XCD x gets the
+  // candidate tiles cb = x (mod 8) and walks them row tile by row tile: its ~64 resident workgroups share
+  // 8 W panels and 8 K* panels through one L2.
+  const int b = blockIdx.x;
+  int I, cb;
+  if ((ncb & 7) == 0) {
+    const int x = b & 7, l = b >> 3, per = ncb >> 3;
+    I = nI - 1 - l / per;
+    cb = 8 * (l % per) + x;
+  } else {
+    I = nI - 1 - b / ncb;
+    cb = b % ncb;
+  }
   const double* Ab = W + (int64_t)I * TT;            // A(m=i,k) = W[k][I*128 + i]
   const double* Bb = kstar + (int64_t)cb * TT;       // B(k,n=c) = K*[k][cb*128 + c]
   TrmmTile tile;
@@ -366,8 +378,8 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
   }
   {
     LaunchTimer tm(c, GPX_TIMER_TRMM);
-    dim3 g((int)((m_chunk + TT - 1) / TT), nI);
-    trmm_sumsq_kernel<<<g, WG, 0, c->stream>>>(W, ldw, b.kstar, C, nI, b.ss_part);
+    const int ncbt = (int)((m_chunk + TT - 1) / TT);
+    trmm_sumsq_kernel<<<ncbt * nI, WG, 0, c->stream>>>(W, ldw, b.kstar, C, nI, ncbt, b.ss_part);
   }
   {
     LaunchTimer tm(c, GPX_TIMER_ACQ);
