@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--kernel", default="rbf")
     ap.add_argument("--acq", default="logei")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--problems-per-gpu", type=int, default=1,
+                    help="independent problems (restarts/seeds) per GPU per step; 4 at 8 GPUs = BASELINE configs[3]")
     ap.add_argument("--cpu-sample", type=int, default=8192, help="candidates in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -107,23 +109,36 @@ def main():
     args = parse()
     dist, rank, world, local = dist_setup(args)
     dev = torch.device("cuda", local)
-    seed = args.seed + 1000 * rank
-    X_np, y_np = synthetic.problem(args.n, args.d, seed)
-    Xs_np = synthetic.sobol(args.m, args.d, seed + 1)
+    P = args.problems_per_gpu
     ls = botorch_default_lengthscale(args.d)
     params = KernelParams(args.kernel, ls, noise=1e-4)
-    X = torch.tensor(X_np, device=dev)
-    y = torch.tensor(y_np, device=dev)
-    Xs = torch.tensor(Xs_np, device=dev)
-    best_f = float(y_np.max())
     eng = GPEngine(dev)
-    state = eng.fit(X, y, params)  # allocation + first-touch outside the timed region
+    probs = []  # (X, y, Xs, best_f, state, global unit index)
+    for q in range(P):
+        unit = rank * P + q
+        seed = args.seed + 1000 * unit
+        X_np, y_np = synthetic.problem(args.n, args.d, seed)
+        Xs_np = synthetic.sobol(args.m, args.d, seed + 1)
+        X, y = torch.tensor(X_np, device=dev), torch.tensor(y_np, device=dev)
+        Xs = torch.tensor(Xs_np, device=dev)
+        state = eng.fit(X, y, params)  # allocation + first-touch outside the timed region
+        probs.append((X, y, Xs, float(y_np.max()), state, unit))
+    X_np, y_np = synthetic.problem(args.n, args.d, args.seed + 1000 * rank * P)  # cpu-baseline inputs
+    Xs_np = synthetic.sobol(args.m, args.d, args.seed + 1000 * rank * P + 1)
+    state = probs[0][4]
+    X, y = probs[0][0], probs[0][1]
     gather_v = torch.empty((world,), dtype=torch.float64, device=dev)
     gather_i = torch.empty((world,), dtype=torch.int64, device=dev)
+    loc_v = torch.empty((P,), dtype=torch.float64, device=dev)
+    loc_i = torch.empty((P,), dtype=torch.int64, device=dev)
 
     def step():
-        st = eng.fit(X, y, params, check=False, out=state)
-        bv, bi = eng.acquire(st, Xs, args.acq, best_f=best_f, index_offset=rank * args.m)
+        for q, (Xq, yq, Xsq, bfq, stq, unit) in enumerate(probs):
+            st = eng.fit(Xq, yq, params, check=False, out=stq)
+            bv, bi = eng.acquire(st, Xsq, args.acq, best_f=bfq, index_offset=unit * args.m)
+            loc_v[q:q + 1].copy_(bv)
+            loc_i[q:q + 1].copy_(bi)
+        bv, bi = eng.argmax_combine(loc_v, loc_i) if P > 1 else (loc_v[:1], loc_i[:1])
         if dist is not None:
             dist.all_gather_into_tensor(gather_v, bv)
             dist.all_gather_into_tensor(gather_i, bi)
@@ -142,7 +157,7 @@ def main():
     elapsed = time.perf_counter() - t0
     trmm_ms, trmm_launches = eng.timing_query("trmm")
     eng.timing_disable()
-    if int(state.info.item()) != 0:
+    if any(int(p[4].info.item()) != 0 for p in probs):
         raise RuntimeError("Cholesky failed inside the benchmark")
 
     # fit-only loop: posterior updates per second
@@ -160,9 +175,9 @@ def main():
 
     if rank == 0:
         m, n = args.m, args.n
-        value = world * m * args.steps / elapsed
+        value = world * P * m * args.steps / elapsed
         avg_ms = trmm_ms / max(trmm_launches, 1)
-        cands_per_launch = m * args.steps / max(trmm_launches, 1)
+        cands_per_launch = P * m * args.steps / max(trmm_launches, 1)
         flops_per_launch = float(n) * n * cands_per_launch  # n^2 flops per candidate (v = L^-1 k*)
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
         cpu = None
@@ -182,10 +197,13 @@ def main():
             "dtype": "f64",
             "data": "synthetic (seeded U[0,1] X, sin-sum y, scrambled Sobol candidates; fixed hyperparameters)",
             "config": {
-                "workload": f"BASELINE configs[1]: n={n} d={args.d} {args.kernel.upper()} GP fp64, one posterior "
-                            f"update + {m}-candidate {args.acq} sweep + argmax per step, per GPU",
+                "workload": (f"BASELINE configs[1]: n={n} d={args.d} {args.kernel.upper()} GP fp64, one posterior "
+                         f"update + {m}-candidate {args.acq} sweep + argmax per step, per GPU") if P == 1 else
+                        (f"BASELINE configs[3] shape: {P} independent n={n} d={args.d} {args.kernel.upper()} problems "
+                         f"per GPU ({P * world} total), each a posterior update + {m}-candidate {args.acq} sweep"),
                 "n": n, "d": args.d, "m": m, "kernel": args.kernel, "acq": args.acq,
-                "parallelism": f"{world} independent problems (one per GPU), RCCL 16-byte argmax all-gather",
+                "parallelism": f"{world * P} independent problems ({P} per GPU), RCCL 16-byte argmax all-gather",
+                "problems_per_gpu": P,
             },
             "updates_per_s": world * args.steps / fit_elapsed,
             "fit_ms": 1e3 * fit_elapsed / args.steps,
