@@ -24,7 +24,11 @@ STATUS_NAMES = {0: "OK", 1: "NOT_PD", 2: "INVALID_ARG", 3: "HIP_ERROR", 4: "RCCL
 
 KERNEL_RBF, KERNEL_MATERN52, KERNEL_SCALE_LINEAR_MATERN52 = 0, 1, 2
 ACQ_EI, ACQ_LOGEI, ACQ_UCB, ACQ_VARIANCE = 0, 1, 2, 3
-TIMERS = {"gram": 0, "potrf": 1, "trtri": 2, "alpha": 3, "kstar": 4, "trmm": 5, "acq": 6}
+TIMERS = {"gram": 0, "potrf": 1, "trtri": 2, "alpha": 3, "kstar": 4, "trmm": 5, "acq": 6, "mll": 7}
+
+# gpx_mll_grad_f64 output layout (include/gpx.h)
+MLL_NLL, MLL_QUAD, MLL_LOGDET, MLL_D_NOISE, MLL_D_OUTPUTSCALE, MLL_D_MEAN = 0, 1, 2, 3, 4, 5
+MLL_D_LENGTHSCALE, MLL_D_LINVAR, MLL_NOUT = 8, 40, 72
 
 
 class GPXLibraryError(RuntimeError):
@@ -100,6 +104,9 @@ _PROTOS = {
                                          c_int64, c_int64, POINTER(AcqParamsC), c_int64, _p, _p, _p, _p,
                                          c_size_t]),
     "gpx_argmax_combine_f64": (c_int32, [_h, _p, _p, c_int64, _p, _p]),
+    "gpx_mll_workspace_size": (c_int32, [c_int64, POINTER(c_size_t)]),
+    "gpx_mll_grad_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, _p, c_int64, _p,
+                                   c_int64, _p, _p, _p, c_size_t]),
     "gpx_timing_enable": (c_int32, [_h, c_int32]),
     "gpx_timing_reset": (c_int32, [_h]),
     "gpx_timing_query": (c_int32, [_h, c_int32, POINTER(c_double), POINTER(c_int64)]),

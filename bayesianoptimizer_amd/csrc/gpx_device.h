@@ -104,6 +104,13 @@ struct MfmaTile {
     }
   }
 
+  // LDS column of element (m, k) of a row-major (not k-major) operand.  Its k-major transpose is written with
+  // scalar ds_write_b64: a 16-lane write group holds 8 k-rows x 2 m, and with row pitch = 16 mod 32 doubles
+  // all 8 k-rows land on one bank pair (8-way conflict, the MFMA loop then waits on LDS stores).  XOR-ing m
+  // with (k & 14) spreads them over all 32 banks; the MFMA fragment reads (16 consecutive m of one k-row per
+  // 16 lanes) only permute inside an aligned 16-block, so they stay conflict-free.
+  __device__ __forceinline__ static int swz(int m, int k) { return m ^ (k & 14); }
+
   // registers -> LDS buffer
   __device__ __forceinline__ void store_lds(double* sA, double* sB) {
     const int t = threadIdx.x;
@@ -115,8 +122,9 @@ struct MfmaTile {
         *reinterpret_cast<double2*>(sA + kk * PA + mm) = ra[q];
       } else {
         int mm = e / BK, kk = e % BK;
-        sA[kk * PA + mm] = ra[q].x;
-        sA[(kk + 1) * PA + mm] = ra[q].y;
+        const int c = swz(mm, kk);
+        sA[kk * PA + c] = ra[q].x;
+        sA[(kk + 1) * PA + c] = ra[q].y;
       }
     }
 #pragma unroll
@@ -127,8 +135,9 @@ struct MfmaTile {
         *reinterpret_cast<double2*>(sB + kk * PB + nn) = rb[q];
       } else {
         int nn = e / BK, kk = e % BK;
-        sB[kk * PB + nn] = rb[q].x;
-        sB[(kk + 1) * PB + nn] = rb[q].y;
+        const int c = swz(nn, kk);
+        sB[kk * PB + c] = rb[q].x;
+        sB[(kk + 1) * PB + c] = rb[q].y;
       }
     }
   }
@@ -139,10 +148,12 @@ struct MfmaTile {
     const int wm0 = (w >> 1) * (TM / 2);
     const int wn0 = (w & 1) * (TN / 2);
     const int kr = lane >> 4, cl = lane & 15;
+    const int row = ks + kr;
+    const int xa = A_KMAJOR ? 0 : (row & 14), xb = B_KMAJOR ? 0 : (row & 14);
 #pragma unroll
-    for (int i = 0; i < WM; ++i) a[i] = sA[(ks + kr) * PA + wm0 + 16 * i + cl];
+    for (int i = 0; i < WM; ++i) a[i] = sA[row * PA + ((wm0 + 16 * i + cl) ^ xa)];
 #pragma unroll
-    for (int j = 0; j < WN; ++j) b[j] = sB[(ks + kr) * PB + wn0 + 16 * j + cl];
+    for (int j = 0; j < WN; ++j) b[j] = sB[row * PB + ((wn0 + 16 * j + cl) ^ xb)];
   }
 
   __device__ __forceinline__ void mm(const double* a, const double* b) {

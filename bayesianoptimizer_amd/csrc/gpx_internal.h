@@ -69,6 +69,11 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
 hipError_t launch_argmax_final(Context* c, const double* vals, const int64_t* idx, int64_t count, double* best_val,
                                int64_t* best_idx);
 
+size_t mll_workspace_bytes(int64_t npad);
+hipError_t launch_mll(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
+                      const double* y, int64_t incy, const double* L, int64_t ldl, const double* W, int64_t ldw,
+                      const double* alpha, double* out, double* part);
+
 int64_t sweep_chunk_size(int64_t npad, int64_t m);
 size_t sweep_workspace_bytes(int64_t npad, int64_t nrhs, int64_t m);
 

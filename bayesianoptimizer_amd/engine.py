@@ -336,6 +336,52 @@ class GPEngine:
                                                     _ptr(bi)))
         return bv, bi
 
+    # -- marginal likelihood ----------------------------------------------------
+    def mll_grad(self, state: GPState, y, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """-log p(y) and its hyperparameter gradient for a fitted single-output state, as a device vector of
+        MLL_NOUT doubles (layout ``_capi.MLL_*``).  Asynchronous."""
+        y = self._as_f64(y, "y")
+        if y.shape != (state.n, 1):
+            raise ValueError(f"y must have shape ({state.n},) or ({state.n}, 1), got {tuple(y.shape)}")
+        if out is None:
+            out = torch.empty((_capi.MLL_NOUT,), dtype=torch.float64, device=self.device)
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_mll_workspace_size(state.n, ctypes.byref(nbytes)))
+        ws = self.workspace("mll", nbytes.value)
+        pc = state.params.to_c(state.d)
+        self._bind_stream()
+        self._check(self.lib.gpx_mll_grad_f64(
+            self.handle, ctypes.byref(pc), state.n, _ptr(state.X), state.X.stride(0), _ptr(y), y.stride(0),
+            _ptr(state.L), state.npad, _ptr(state.W), state.npad, _ptr(state.alpha), _ptr(out), _ptr(ws),
+            ws.numel()))
+        return out
+
+    def mll_value_grad(self, X, y, params: KernelParams, jitters: Sequence[float] = (0.0, 1e-8, 1e-7, 1e-6),
+                       state: Optional[GPState] = None):
+        """Fit at ``params`` (retrying with the psd_safe_cholesky jitter ladder [upstream] on NOT_PD) and return
+        (host dict of -log p(y) and its gradient w.r.t. the natural hyperparameters, state).  Synchronises."""
+        X = self._as_f64(X, "X")
+        y = self._as_f64(y, "y")
+        err = None
+        for jit in jitters:
+            try:
+                state = self.fit(X, y, params.replace(jitter=params.jitter + jit), out=state)
+                break
+            except NotPositiveDefiniteError as e:
+                err = e
+        else:
+            raise err
+        v = self.mll_grad(state, y).cpu().numpy()
+        d = X.shape[1]
+        res = {
+            "nll": float(v[_capi.MLL_NLL]), "quad": float(v[_capi.MLL_QUAD]), "logdet": float(v[_capi.MLL_LOGDET]),
+            "noise": float(v[_capi.MLL_D_NOISE]), "outputscale": float(v[_capi.MLL_D_OUTPUTSCALE]),
+            "const_mean": float(v[_capi.MLL_D_MEAN]),
+            "lengthscale": v[_capi.MLL_D_LENGTHSCALE:_capi.MLL_D_LENGTHSCALE + d].copy(),
+            "linear_variance": v[_capi.MLL_D_LINVAR:_capi.MLL_D_LINVAR + d].copy(),
+        }
+        return res, state
+
     # -- instrumentation ------------------------------------------------------------------------
     def timing_enable(self, timers: Sequence[str] = ("trmm",)):
         mask = 0

@@ -65,7 +65,22 @@ enum {
   GPX_TIMER_KSTAR = 4,
   GPX_TIMER_TRMM = 5,
   GPX_TIMER_ACQ = 6,
-  GPX_TIMER_COUNT = 7
+  GPX_TIMER_MLL = 7,
+  GPX_TIMER_COUNT = 8
+};
+
+/* Layout of the gpx_mll_grad_f64 output vector (GPX_MLL_NOUT doubles).  Gradients are of the negative log
+ * marginal likelihood w.r.t. the natural (constrained) hyperparameters of gpx_kernel_params. */
+enum {
+  GPX_MLL_NLL = 0,            /* -log p(y) = QUAD + LOGDET/2 + n/2 log(2 pi) */
+  GPX_MLL_QUAD = 1,           /* (y - m)^T K^{-1} (y - m) / 2 */
+  GPX_MLL_LOGDET = 2,         /* log |K| = 2 sum log L_ii */
+  GPX_MLL_D_NOISE = 3,
+  GPX_MLL_D_OUTPUTSCALE = 4,
+  GPX_MLL_D_MEAN = 5,
+  GPX_MLL_D_LENGTHSCALE = 8,  /* GPX_MAX_DIM entries */
+  GPX_MLL_D_LINVAR = 40,      /* GPX_MAX_DIM entries (SCALE_LINEAR_MATERN52 only) */
+  GPX_MLL_NOUT = 72
 };
 
 typedef struct {
@@ -166,6 +181,21 @@ gpx_status gpx_acquire_argmax_f64(gpx_handle h, const gpx_kernel_params* p, int6
  * never wins.  Used after the cross-GPU all-gather of per-rank records. */
 gpx_status gpx_argmax_combine_f64(gpx_handle h, const double* vals, const int64_t* idx, int64_t count,
                                   double* best_val, int64_t* best_idx);
+
+/* ---- marginal likelihood -------------------------------------------------------- */
+/* Negative log marginal likelihood of a fitted exact GP and its gradient:
+ *   d(-log p)/d theta = 1/2 sum_ij (K^{-1} - alpha alpha^T)_ij dK_ij/d theta,   d/dm = -sum_i alpha_i,
+ * with K^{-1} = W W^T formed tile by tile on the MFMA units and contracted against dK/d theta recomputed
+ * from X inside the same kernel (K^{-1} is never stored).  Inputs are the outputs of gpx_fit_f64 for one
+ * output column: L (the factored K), W, alpha (column 0, contiguous padded_n), and the targets y (n, stride
+ * incy) the fit used.  out: device array of GPX_MLL_NOUT doubles (layout above; the covariance is
+ * differentiated in fp64 regardless of cov_fp32).  Deterministic (fixed reduction order).
+ * Replaces ExactMarginalLogLikelihood(...).backward() inside fit_gpytorch_mll [upstream]
+ * (optimization/Bayesian.py:92-93, optimization/Bayesian1.py:114-115, optimization/Bayesian6.py:480-488). */
+gpx_status gpx_mll_workspace_size(int64_t n, size_t* bytes);
+gpx_status gpx_mll_grad_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                            const double* y, int64_t incy, const double* L, int64_t ldl, const double* W,
+                            int64_t ldw, const double* alpha, double* out, void* ws, size_t ws_bytes);
 
 /* ---- instrumentation ------------------------------------------------------------------------------ */
 /* For every timer whose bit is set in `mask`, each launch of that kernel family is bracketed by hipEvents

@@ -23,6 +23,7 @@ What it restates (fp64, NumPy/SciPy):
       the variance-sum pool scan is ``optimization/Bayesian7.py:664-671``).
 * a8  Argmax with the lowest index winning ties (``optimization/Bayesian.py:117``,
       ``optimization/Bayesian7.py:681,724-727``).
+* §8f row 1: -log p(y) and its gradient w.r.t. the kernel hyperparameters (``mll_value_grad``).
 * a1/a2 input/output transforms of ``optimization/Bayesian7.py:181-190,363-385``.
 
 Parity status: **parity unpinned**.  The reference delegates this arithmetic to GPyTorch /
@@ -198,6 +199,70 @@ def fit(X: np.ndarray, y: np.ndarray, p: KernelParams) -> GPState:
     L = cholesky(K)
     alpha = sla.cho_solve((L, True), y - p.const_mean, check_finite=False)
     return GPState(X=X, L=L, alpha=alpha, params=p)
+
+
+# ---------------------------------------------------------------------------------------------
+# §8f row 1: negative log marginal likelihood and its hyperparameter gradient
+# ---------------------------------------------------------------------------------------------
+def kernel_grads(X: np.ndarray, p: KernelParams) -> dict:
+    """dK/d theta (n x n each, noise excluded) for the natural hyperparameters of ``p`` (fp64).
+
+    RBF  k = s exp(-r^2/2):                 dk/dl_k = k q_k / l_k,  dk/ds = exp(-r^2/2)
+    M52  k = s (1+sqrt5 r+5r^2/3) e^{-sqrt5 r}: dk/dl_k = s (5/3)(1+sqrt5 r) e^{-sqrt5 r} q_k / l_k,
+                                               dk/ds = (1+sqrt5 r+5r^2/3) e^{-sqrt5 r}
+    +lin k = s (sum_k v_k x_k x'_k + M52):   dk/dv_k = s x_k x'_k,  dk/ds += sum_k v_k x_k x'_k
+    with q_k = ((x_k - x'_k) / l_k)^2 (GPyTorch RBFKernel / MaternKernel / LinearKernel / ScaleKernel [upstream]).
+    """
+    X = np.asarray(X, dtype=np.float64)
+    ls = p.lengthscale
+    q = [((X[:, k:k + 1] - X[None, :, k]) / ls[k]) ** 2 for k in range(X.shape[1])]
+    r2 = np.zeros_like(q[0])
+    for qk in q:
+        r2 += qk
+    if p.kind == RBF:
+        base = np.exp(-0.5 * r2)
+        kfac = p.outputscale * base
+    else:
+        r = np.sqrt(r2)
+        ex = np.exp(-math.sqrt(5.0) * r)
+        base = (1.0 + math.sqrt(5.0) * r + (5.0 / 3.0) * r2) * ex
+        kfac = p.outputscale * (5.0 / 3.0) * (1.0 + math.sqrt(5.0) * r) * ex
+    out = {"lengthscale": [kfac * q[k] / ls[k] for k in range(X.shape[1])]}
+    if p.kind == SCALE_LINEAR_MATERN52:
+        out["linear_variance"] = [p.outputscale * np.outer(X[:, k], X[:, k]) for k in range(X.shape[1])]
+        base = base + (X * p.linear_variance) @ X.T
+    out["outputscale"] = base
+    return out
+
+
+def mll_value_grad(X: np.ndarray, y: np.ndarray, p: KernelParams) -> dict:
+    """-log p(y) = 1/2 (y-m)^T alpha + sum log L_ii + n/2 log 2pi and its gradient
+    1/2 sum_ij (K^{-1} - alpha alpha^T)_ij dK_ij/d theta, d/dm = -sum alpha (the quantity
+    ExactMarginalLogLikelihood differentiates inside fit_gpytorch_mll [upstream], reached from
+    optimization/Bayesian.py:92-93, optimization/Bayesian6.py:480-488), before the 1/n scaling and priors."""
+    X = np.asarray(X, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64).reshape(-1)
+    n = X.shape[0]
+    st = fit(X, y, p)
+    L, alpha = st.L, st.alpha
+    quad = 0.5 * float((y - p.const_mean) @ alpha)
+    logdet = 2.0 * float(np.log(np.diag(L)).sum())
+    Kinv = sla.cho_solve((L, True), np.eye(n), check_finite=False)
+    G = 0.5 * (Kinv - np.outer(alpha, alpha))
+    dk = kernel_grads(X, p)
+    d = X.shape[1]
+    res = {
+        "nll": quad + 0.5 * logdet + 0.5 * n * math.log(2.0 * math.pi),
+        "quad": quad,
+        "logdet": logdet,
+        "noise": float(np.trace(G)),
+        "outputscale": float((G * dk["outputscale"]).sum()),
+        "const_mean": -float(alpha.sum()),
+        "lengthscale": np.array([(G * dk["lengthscale"][k]).sum() for k in range(d)]),
+        "linear_variance": (np.array([(G * dk["linear_variance"][k]).sum() for k in range(d)])
+                            if p.kind == SCALE_LINEAR_MATERN52 else np.zeros(d)),
+    }
+    return res
 
 
 # ---------------------------------------------------------------------------------------------
