@@ -105,8 +105,8 @@ _PROTOS = {
                                          c_size_t]),
     "gpx_argmax_combine_f64": (c_int32, [_h, _p, _p, c_int64, _p, _p]),
     "gpx_mll_workspace_size": (c_int32, [c_int64, POINTER(c_size_t)]),
-    "gpx_mll_grad_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, _p, c_int64, _p,
-                                   c_int64, _p, _p, _p, c_size_t]),
+    "gpx_mll_grad_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, c_int64, _p,
+                                   c_int64, _p, c_int64, _p, _p, _p, c_size_t]),
     "gpx_timing_enable": (c_int32, [_h, c_int32]),
     "gpx_timing_reset": (c_int32, [_h]),
     "gpx_timing_query": (c_int32, [_h, c_int32, POINTER(c_double), POINTER(c_int64)]),

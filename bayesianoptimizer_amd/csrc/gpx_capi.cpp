@@ -280,14 +280,15 @@ gpx_status gpx_mll_workspace_size(int64_t n, size_t* bytes) {
 }
 
 gpx_status gpx_mll_grad_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
-                            const double* y, int64_t incy, const double* L, int64_t ldl, const double* W,
-                            int64_t ldw, const double* alpha, double* out, void* ws, size_t ws_bytes) {
+                            const double* Y, int64_t ldy, int64_t nrhs, const double* L, int64_t ldl,
+                            const double* W, int64_t ldw, const double* alpha, double* out, void* ws,
+                            size_t ws_bytes) {
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return GPX_INVALID_ARG;
   GPX_TRY(check_params(c, p));
   GPX_TRY(check_n(c, n));
   GPX_NONNULL(c, X);
-  GPX_NONNULL(c, y);
+  GPX_NONNULL(c, Y);
   GPX_NONNULL(c, L);
   GPX_NONNULL(c, W);
   GPX_NONNULL(c, alpha);
@@ -297,10 +298,11 @@ gpx_status gpx_mll_grad_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n,
   GPX_TRY(check_ld(c, ldx, p->d, "X", false));
   GPX_TRY(check_ld(c, ldl, npad, "L", false));
   GPX_TRY(check_ld(c, ldw, npad, "W", true));
-  if (incy < 1) return fail(c, GPX_INVALID_ARG, "incy must be >= 1");
+  if (nrhs < 1 || nrhs > GPX_MAX_RHS) return fail(c, GPX_INVALID_ARG, "nrhs must be in [1, 8]");
+  GPX_TRY(check_ld(c, ldy, nrhs, "Y", false));
   if (ws_bytes < gpx::mll_workspace_bytes(npad) + 256) return fail(c, GPX_INVALID_ARG, "mll workspace too small");
   GPX_TRY(use_device(c));
-  return hip_check(c, gpx::launch_mll(c, *p, (int)n, (int)npad, X, ldx, y, incy, L, ldl, W, ldw, alpha, out,
+  return hip_check(c, gpx::launch_mll(c, *p, (int)n, (int)npad, X, ldx, Y, ldy, (int)nrhs, L, ldl, W, ldw, alpha, out,
                                       align256(ws)), "mll");
 }
 

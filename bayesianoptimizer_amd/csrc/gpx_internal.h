@@ -71,8 +71,8 @@ hipError_t launch_argmax_final(Context* c, const double* vals, const int64_t* id
 
 size_t mll_workspace_bytes(int64_t npad);
 hipError_t launch_mll(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
-                      const double* y, int64_t incy, const double* L, int64_t ldl, const double* W, int64_t ldw,
-                      const double* alpha, double* out, double* part);
+                      const double* Y, int64_t ldy, int nrhs, const double* L, int64_t ldl, const double* W,
+                      int64_t ldw, const double* alpha, double* out, double* part);
 
 int64_t sweep_chunk_size(int64_t npad, int64_t m);
 size_t sweep_workspace_bytes(int64_t npad, int64_t nrhs, int64_t m);

@@ -2,8 +2,9 @@
 // (replaces ExactMarginalLogLikelihood(...).backward() inside fit_gpytorch_mll [upstream],
 // optimization/Bayesian.py:92-93, optimization/Bayesian1.py:114-115, optimization/Bayesian6.py:480-488).
 //
-//   -log p(y) = 1/2 (y-m)^T alpha + sum_i log L_ii + n/2 log(2 pi)
-//   d/d theta = 1/2 sum_ij (K^{-1} - alpha alpha^T)_ij dK_ij/d theta
+//   -log p(Y) = sum_t [ 1/2 (y_t-m)^T alpha_t + sum_i log L_ii + n/2 log(2 pi) ]
+//   d/d theta = 1/2 sum_ij (T K^{-1} - sum_t alpha_t alpha_t^T)_ij dK_ij/d theta
+// for T = nrhs outputs sharing the covariance (T = 1: the SingleTaskGP objective).
 //
 // mll_grad_kernel: one workgroup per lower 128x128 tile (I >= J) of K^{-1} = W W^T (W = L^{-T} upper,
 // row-major: W[i][k] != 0 only for k >= i, so the k loop of tile (I, J) starts at I*128).  The tile is
@@ -35,12 +36,13 @@ template <int DMAX>
 __global__ void __launch_bounds__(WG) mll_grad_kernel(gpx_kernel_params p, int n, int npad,
                                                       const double* __restrict__ X, int64_t ldx,
                                                       const double* __restrict__ W, int64_t ldw,
-                                                      const double* __restrict__ alpha, int kc,
+                                                      const double* __restrict__ alpha, int nrhs, int kc,
                                                       double* __restrict__ part) {
   using Tile = MfmaTile<MT, MT, 16, false, false>;
-  // Epilogue LDS: raw X rows of both tile sides, their alpha, and one 128 x SW slab of the K^{-1} tile.
-  constexpr int SW = 32, KVP = SW + 1, XP = DMAX + 1;
-  constexpr int EPI = 2 * MT * XP + 2 * MT + MT * KVP;
+  // Epilogue LDS: raw X rows of both tile sides, their alpha rows (<= GPX_MAX_RHS outputs), and one 128 x SW
+  // slab of the K^{-1} tile.
+  constexpr int SW = 16, KVP = SW + 1, XP = DMAX + 1;
+  constexpr int EPI = 2 * MT * XP + 2 * MT * GPX_MAX_RHS + MT * KVP;
   constexpr int SMEM = EPI > Tile::LDS_DOUBLES ? EPI : Tile::LDS_DOUBLES;  // 73.7 KB for d <= 16
   __shared__ __attribute__((aligned(16))) double smem[SMEM];
   int I, J;
@@ -63,19 +65,20 @@ __global__ void __launch_bounds__(WG) mll_grad_kernel(gpx_kernel_params p, int n
   // ---- epilogue: stage raw X rows and alpha of both tile sides in LDS
   double* xi = smem;             // [MT][XP]
   double* xj = xi + MT * XP;     // [MT][XP]
-  double* ai = xj + MT * XP;     // [MT]
-  double* aj = ai + MT;          // [MT]
-  double* kv = aj + MT;          // [MT][KVP]
+  double* ai = xj + MT * XP;                // [MT][nrhs]
+  double* aj = ai + MT * GPX_MAX_RHS;       // [MT][nrhs]
+  double* kv = aj + MT * GPX_MAX_RHS;       // [MT][KVP]
   const int d = p.d;
   for (int e = threadIdx.x; e < MT * DMAX; e += WG) {
     const int r = e / DMAX, k = e % DMAX;
     xi[r * XP + k] = (k < d && i0 + r < n) ? X[(int64_t)(i0 + r) * ldx + k] : 0.0;
     xj[r * XP + k] = (k < d && j0 + r < n) ? X[(int64_t)(j0 + r) * ldx + k] : 0.0;
   }
-  for (int e = threadIdx.x; e < MT; e += WG) {
-    ai[e] = alpha[i0 + e];
-    aj[e] = alpha[j0 + e];
+  for (int e = threadIdx.x; e < MT * nrhs; e += WG) {
+    ai[e] = alpha[(int64_t)i0 * nrhs + e];
+    aj[e] = alpha[(int64_t)j0 * nrhs + e];
   }
+  const double tk = (double)nrhs;
 
   const int kind = p.kind;
   const bool lin = (kind == GPX_KERNEL_SCALE_LINEAR_MATERN52);
@@ -89,18 +92,15 @@ __global__ void __launch_bounds__(WG) mll_grad_kernel(gpx_kernel_params p, int n
   double gs = 0.0, gn = 0.0;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 
-  // Four 32-column slabs: the two waves owning the slab's columns park their accumulators in LDS, then all
+  // Eight 16-column slabs: the two waves owning the slab's columns park their accumulators in LDS, then all
   // 256 threads contract the slab element by element (a rolled loop keeps register pressure flat).
 #pragma unroll
   for (int sl = 0; sl < MT / SW; ++sl) {
-    if ((w & 1) == (sl >> 1)) {
+    if ((w & 1) == (sl >> 2)) {
 #pragma unroll
       for (int a = 0; a < Tile::WM; ++a)
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            kv[Tile::row_of(a, r) * KVP + 16 * jj + (lane & 15)] = t.acc[a][2 * (sl & 1) + jj][r];
+        for (int r = 0; r < 4; ++r) kv[Tile::row_of(a, r) * KVP + (lane & 15)] = t.acc[a][sl & 3][r];
     }
     __syncthreads();
 #pragma unroll 1
@@ -108,8 +108,10 @@ __global__ void __launch_bounds__(WG) mll_grad_kernel(gpx_kernel_params p, int n
       const int ri = e / SW, cj = e % SW;
       const int gi = i0 + ri, gj = j0 + sl * SW + cj;
       if (gi >= n || gj >= n || gj > gi) continue;
-      // G = (K^{-1} - alpha alpha^T)_ij, weighted so that summing the lower triangle gives 1/2 sum_ij
-      const double G = ((gi == gj) ? 0.5 : 1.0) * (kv[ri * KVP + cj] - aa * ai[ri] * aj[sl * SW + cj]);
+      // G = (T K^{-1} - sum_t alpha_t alpha_t^T)_ij, weighted so that summing the lower triangle gives 1/2 sum_ij
+      double aat = 0.0;
+      for (int q = 0; q < nrhs; ++q) aat += ai[ri * nrhs + q] * aj[(sl * SW + cj) * nrhs + q];
+      const double G = ((gi == gj) ? 0.5 : 1.0) * (tk * kv[ri * KVP + cj] - aa * aat);
       const double* x1 = xi + ri * XP;
       const double* x2 = xj + (sl * SW + cj) * XP;
       double q[DMAX];
@@ -201,8 +203,8 @@ __global__ void __launch_bounds__(WG) mll_rowsum_kernel(const double* __restrict
 
 // Single workgroup: the O(n) terms (quadratic form, log-determinant, mean gradient) on top of the summed
 // gradient row.
-__global__ void __launch_bounds__(WG) mll_finalize_kernel(int n, const double* __restrict__ gsum,
-                                                          const double* __restrict__ y, int64_t incy,
+__global__ void __launch_bounds__(WG) mll_finalize_kernel(int n, int nrhs, const double* __restrict__ gsum,
+                                                          const double* __restrict__ Y, int64_t ldy,
                                                           const double* __restrict__ L, int64_t ldl,
                                                           const double* __restrict__ alpha, double const_mean,
                                                           double* __restrict__ out) {
@@ -220,10 +222,12 @@ __global__ void __launch_bounds__(WG) mll_finalize_kernel(int n, const double* _
   };
   double q = 0.0, ld = 0.0, sa = 0.0;
   for (int i = threadIdx.x; i < n; i += WG) {
-    const double a = alpha[i];
-    q += (y[(int64_t)i * incy] - const_mean) * a;
+    for (int t = 0; t < nrhs; ++t) {
+      const double a = alpha[(int64_t)i * nrhs + t];
+      q += (Y[(int64_t)i * ldy + t] - const_mean) * a;
+      sa += a;
+    }
     ld += log(L[(int64_t)i * ldl + i]);
-    sa += a;
   }
   q = block_sum(q);
   ld = block_sum(ld);
@@ -232,7 +236,7 @@ __global__ void __launch_bounds__(WG) mll_finalize_kernel(int n, const double* _
     double v = gsum[o];
     if (o == GPX_MLL_QUAD) v = 0.5 * q;
     if (o == GPX_MLL_LOGDET) v = 2.0 * ld;
-    if (o == GPX_MLL_NLL) v = 0.5 * q + ld + 0.5 * (double)n * LOG_2PI;
+    if (o == GPX_MLL_NLL) v = 0.5 * q + (double)nrhs * (ld + 0.5 * (double)n * LOG_2PI);
     if (o == GPX_MLL_D_MEAN) v = -sa;
     if (o == 6 || o == 7) v = 0.0;
     out[o] = v;
@@ -253,21 +257,21 @@ size_t mll_workspace_bytes(int64_t npad) {
 }
 
 hipError_t launch_mll(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
-                      const double* y, int64_t incy, const double* L, int64_t ldl, const double* W, int64_t ldw,
-                      const double* alpha, double* out, double* part) {
+                      const double* Y, int64_t ldy, int nrhs, const double* L, int64_t ldl, const double* W,
+                      int64_t ldw, const double* alpha, double* out, double* part) {
   LaunchTimer tm(c, GPX_TIMER_MLL);
   const int T = npad / MT;
   const int tiles = T * (T + 1) / 2;
   const int kc = mll_kchunk(npad);
   const dim3 grid(tiles, (npad + kc - 1) / kc);
   if (p.d <= 4)
-    mll_grad_kernel<4><<<grid, WG, 0, c->stream>>>(p, n, npad, X, ldx, W, ldw, alpha, kc, part);
+    mll_grad_kernel<4><<<grid, WG, 0, c->stream>>>(p, n, npad, X, ldx, W, ldw, alpha, nrhs, kc, part);
   else if (p.d <= 8)
-    mll_grad_kernel<8><<<grid, WG, 0, c->stream>>>(p, n, npad, X, ldx, W, ldw, alpha, kc, part);
+    mll_grad_kernel<8><<<grid, WG, 0, c->stream>>>(p, n, npad, X, ldx, W, ldw, alpha, nrhs, kc, part);
   else if (p.d <= 16)
-    mll_grad_kernel<16><<<grid, WG, 0, c->stream>>>(p, n, npad, X, ldx, W, ldw, alpha, kc, part);
+    mll_grad_kernel<16><<<grid, WG, 0, c->stream>>>(p, n, npad, X, ldx, W, ldw, alpha, nrhs, kc, part);
   else
-    mll_grad_kernel<32><<<grid, WG, 0, c->stream>>>(p, n, npad, X, ldx, W, ldw, alpha, kc, part);
+    mll_grad_kernel<32><<<grid, WG, 0, c->stream>>>(p, n, npad, X, ldx, W, ldw, alpha, nrhs, kc, part);
   const int64_t rows = (int64_t)tiles * grid.y;
   const int64_t rpb = std::max<int64_t>(64, (rows + 255) / 256);
   const int nb = (int)((rows + rpb - 1) / rpb);
@@ -275,7 +279,7 @@ hipError_t launch_mll(Context* c, const gpx_kernel_params& p, int n, int npad, c
   double* gsum = stage + 256 * GPX_MLL_NOUT;
   mll_rowsum_kernel<<<nb, WG, 0, c->stream>>>(part, rows, rpb, stage);
   mll_rowsum_kernel<<<1, WG, 0, c->stream>>>(stage, nb, nb, gsum);
-  mll_finalize_kernel<<<1, WG, 0, c->stream>>>(n, gsum, y, incy, L, ldl, alpha, p.const_mean, out);
+  mll_finalize_kernel<<<1, WG, 0, c->stream>>>(n, nrhs, gsum, Y, ldy, L, ldl, alpha, p.const_mean, out);
   return hipGetLastError();
 }
 

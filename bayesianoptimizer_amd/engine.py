@@ -337,12 +337,12 @@ class GPEngine:
         return bv, bi
 
     # -- marginal likelihood ----------------------------------------------------
-    def mll_grad(self, state: GPState, y, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """-log p(y) and its hyperparameter gradient for a fitted single-output state, as a device vector of
-        MLL_NOUT doubles (layout ``_capi.MLL_*``).  Asynchronous."""
-        y = self._as_f64(y, "y")
-        if y.shape != (state.n, 1):
-            raise ValueError(f"y must have shape ({state.n},) or ({state.n}, 1), got {tuple(y.shape)}")
+    def mll_grad(self, state: GPState, Y, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """-log p(Y) and its gradient w.r.t. the shared hyperparameters of a fitted state (Y: the n x nrhs targets
+        the fit used), as a device vector of MLL_NOUT doubles (layout ``_capi.MLL_*``).  Asynchronous."""
+        Y = self._as_f64(Y, "Y")
+        if Y.shape != (state.n, state.nrhs):
+            raise ValueError(f"Y must have shape ({state.n}, {state.nrhs}), got {tuple(Y.shape)}")
         if out is None:
             out = torch.empty((_capi.MLL_NOUT,), dtype=torch.float64, device=self.device)
         nbytes = ctypes.c_size_t()
@@ -351,15 +351,16 @@ class GPEngine:
         pc = state.params.to_c(state.d)
         self._bind_stream()
         self._check(self.lib.gpx_mll_grad_f64(
-            self.handle, ctypes.byref(pc), state.n, _ptr(state.X), state.X.stride(0), _ptr(y), y.stride(0),
-            _ptr(state.L), state.npad, _ptr(state.W), state.npad, _ptr(state.alpha), _ptr(out), _ptr(ws),
-            ws.numel()))
+            self.handle, ctypes.byref(pc), state.n, _ptr(state.X), state.X.stride(0), _ptr(Y), Y.stride(0),
+            state.nrhs, _ptr(state.L), state.npad, _ptr(state.W), state.npad, _ptr(state.alpha), _ptr(out),
+            _ptr(ws), ws.numel()))
         return out
 
     def mll_value_grad(self, X, y, params: KernelParams, jitters: Sequence[float] = (0.0, 1e-8, 1e-7, 1e-6),
                        state: Optional[GPState] = None):
         """Fit at ``params`` (retrying with the psd_safe_cholesky jitter ladder [upstream] on NOT_PD) and return
-        (host dict of -log p(y) and its gradient w.r.t. the natural hyperparameters, state).  Synchronises."""
+        (host dict of -log p(Y) and its gradient w.r.t. the natural hyperparameters, state).  Y: n or n x T
+        (T outputs sharing the hyperparameters).  Synchronises."""
         X = self._as_f64(X, "X")
         y = self._as_f64(y, "y")
         err = None

@@ -228,18 +228,15 @@ def fit_hyperparameters(engine, X, y, kind: str = "rbf", prior_set: str = "dim_s
     from scipy.optimize import minimize
 
     Xn = np.asarray(X.cpu() if hasattr(X, "cpu") else X, dtype=np.float64)
-    yn = np.asarray(y.cpu() if hasattr(y, "cpu") else y, dtype=np.float64).reshape(-1)
+    yn = np.asarray(y.cpu() if hasattr(y, "cpu") else y, dtype=np.float64)
+    yn = yn.reshape(-1, 1) if yn.ndim == 1 else yn  # T columns share the hyperparameters
     n, d = Xn.shape
     spec = default_spec(kind, d, prior_set, base, fit_mean)
     if value_grad is None:
-        Xd = yd = None
         state = [None]
 
         def value_grad(p):
-            nonlocal Xd, yd
-            if Xd is None:
-                Xd, yd = engine._as_f64(X, "X"), engine._as_f64(yn, "y")
-            res, state[0] = engine.mll_value_grad(Xd, yd, p, state=state[0])
+            res, state[0] = engine.mll_value_grad(X, y, p, state=state[0])
             return res
 
     f = objective(spec, value_grad, n)

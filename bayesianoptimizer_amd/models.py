@@ -9,9 +9,11 @@ These mirror the reference's operator surface for the hot path so calling code r
   LogExpectedImprovement(model, best_f).sweep(X) -> (value, index)     ≙ analytic LogEI + raw-sample argmax
   ExpectedImprovement / UpperConfidenceBound / PosteriorVariance       ≙ the other analytic scores
 
-Hyperparameters are fixed (no MLL fitting; SURVEY §8f row 1 is the next step).  NOT_PD handling follows the
-reference's jitter-retry policy (optimization/Bayesian6.py:481-488): the factorisation is retried with the
-jitters of ``jitter_schedule`` before the NotPositiveDefiniteError propagates.
+Hyperparameters are either given (``params``) or fitted by maximum marginal likelihood with
+``ExactGP.fit_hyperparameters`` (the fit_gpytorch_mll step of optimization/Bayesian.py:92-93,
+objective and gradient on the GPU, L-BFGS-B on the host; see mll.py).  NOT_PD handling follows the reference's
+jitter-retry policy (optimization/Bayesian6.py:481-488): the factorisation is retried with the jitters of
+``jitter_schedule`` before the NotPositiveDefiniteError propagates.
 """
 from __future__ import annotations
 
@@ -21,7 +23,7 @@ from typing import Optional, Sequence
 import torch
 
 from ._capi import NotPositiveDefiniteError
-from .engine import GPEngine, GPState, KernelParams, botorch_default_lengthscale
+from .engine import KERNEL_KINDS, GPEngine, GPState, KernelParams, botorch_default_lengthscale
 from .transforms import Standardize
 
 
@@ -52,6 +54,7 @@ class ExactGP:
         self.jitter_schedule = tuple(jitter_schedule)
         self.state: Optional[GPState] = None
         self.jitter_used = None
+        self.mll_result = None
 
     @property
     def num_outputs(self) -> int:
@@ -74,6 +77,24 @@ class ExactGP:
             except NotPositiveDefiniteError as e:  # reference: retry with larger cholesky_jitter
                 last = e
         raise last
+
+    def fit_hyperparameters(self, prior_set: str = "dim_scaled", fit_mean: bool = True,
+                            options: Optional[dict] = None) -> "ExactGP":
+        """Maximum marginal likelihood over the hyperparameters (all outputs share them), then refit the posterior
+        caches at the optimum.  ``prior_set``: "dim_scaled" (BoTorch >= 0.12 SingleTaskGP), "gamma" (older
+        BoTorch) or "none" (see mll.py)."""
+        from .mll import fit_hyperparameters
+
+        Y = self.train_Y
+        if self.outcome_transform is not None:
+            Y = self.outcome_transform.fit(Y).transform(Y)
+        kind = self.params.kind if isinstance(self.params.kind, str) else \
+            {v: k for k, v in KERNEL_KINDS.items()}[int(self.params.kind)]
+        res = fit_hyperparameters(self.engine, self.train_X, Y, kind, prior_set, base=self.params, fit_mean=fit_mean,
+                                  options=options)
+        self.params = res.params
+        self.mll_result = res
+        return self.fit()
 
     def _untransform(self):
         ot = self.outcome_transform

@@ -50,6 +50,12 @@ class GPConfig:
     noise: float = 1e-3
     jitter_val: float = 1e-4              # Bayesian6.py GPConfig.jitter_val; retried at 1e-2 (:487)
     beta: float = 4.0
+    # hyperparameters: learned each round like the reference's model fit (fit_gpytorch_mll, Bayesian.py:92-93;
+    # the driven variant trains them by ELBO, Bayesian7.py:451-538) — here by exact marginal likelihood on the
+    # GPU (mll.py), starting from the values above; False keeps them fixed
+    fit_hyperparameters: bool = True
+    prior_set: str = "none"               # "none" (ScaleKernel(Linear + Matern) of Bayesian6/7) | "dim_scaled" | "gamma"
+    mll_options: Optional[dict] = None    # scipy L-BFGS-B options
 
 
 class BayesianOptimizer:
@@ -201,7 +207,10 @@ class BayesianOptimizer:
         Ys = self.y_tf(self.train_Y_raw)
         self.gp_model = ExactGP(Xs, Ys, self._kernel_params(), engine=self.engine,
                                 jitter_schedule=(0.0, self.config.jitter_val, 1e-2))
-        self.gp_model.fit()
+        if self.config.fit_hyperparameters:
+            self.gp_model.fit_hyperparameters(self.config.prior_set, options=self.config.mll_options)
+        else:
+            self.gp_model.fit()
         return self.gp_model
 
     def predict(self, x_orig_numpy: np.ndarray, return_var: bool = False):

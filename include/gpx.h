@@ -183,19 +183,22 @@ gpx_status gpx_argmax_combine_f64(gpx_handle h, const double* vals, const int64_
                                   double* best_val, int64_t* best_idx);
 
 /* ---- marginal likelihood -------------------------------------------------------- */
-/* Negative log marginal likelihood of a fitted exact GP and its gradient:
- *   d(-log p)/d theta = 1/2 sum_ij (K^{-1} - alpha alpha^T)_ij dK_ij/d theta,   d/dm = -sum_i alpha_i,
+/* Negative log marginal likelihood of a fitted exact GP with T = nrhs outputs sharing the covariance (T = 1:
+ * the SingleTaskGP objective) and its gradient w.r.t. the shared hyperparameters:
+ *   -log p(Y) = sum_t [ (y_t - m)^T alpha_t / 2 ] + T (sum log L_ii + n/2 log 2 pi)
+ *   d/d theta = 1/2 sum_ij (T K^{-1} - sum_t alpha_t alpha_t^T)_ij dK_ij/d theta,   d/dm = -sum_t sum_i alpha_ti,
  * with K^{-1} = W W^T formed tile by tile on the MFMA units and contracted against dK/d theta recomputed
- * from X inside the same kernel (K^{-1} is never stored).  Inputs are the outputs of gpx_fit_f64 for one
- * output column: L (the factored K), W, alpha (column 0, contiguous padded_n), and the targets y (n, stride
- * incy) the fit used.  out: device array of GPX_MLL_NOUT doubles (layout above; the covariance is
- * differentiated in fp64 regardless of cov_fp32).  Deterministic (fixed reduction order).
- * Replaces ExactMarginalLogLikelihood(...).backward() inside fit_gpytorch_mll [upstream]
- * (optimization/Bayesian.py:92-93, optimization/Bayesian1.py:114-115, optimization/Bayesian6.py:480-488). */
+ * from X inside the same kernel (K^{-1} is never stored).  Inputs are the outputs of gpx_fit_f64: L (the
+ * factored K), W, alpha (contiguous padded_n x nrhs), and the targets Y (n x nrhs, leading dim ldy) the fit
+ * used.  out: device array of GPX_MLL_NOUT doubles (layout above; QUAD and LOGDET are the totals over the
+ * outputs and one log|K|; the covariance is differentiated in fp64 regardless of cov_fp32).  Deterministic
+ * (fixed reduction order).  Replaces ExactMarginalLogLikelihood(...).backward() inside fit_gpytorch_mll
+ * [upstream] (optimization/Bayesian.py:92-93, optimization/Bayesian1.py:114-115, optimization/Bayesian6.py:480-488). */
 gpx_status gpx_mll_workspace_size(int64_t n, size_t* bytes);
 gpx_status gpx_mll_grad_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
-                            const double* y, int64_t incy, const double* L, int64_t ldl, const double* W,
-                            int64_t ldw, const double* alpha, double* out, void* ws, size_t ws_bytes);
+                            const double* Y, int64_t ldy, int64_t nrhs, const double* L, int64_t ldl,
+                            const double* W, int64_t ldw, const double* alpha, double* out, void* ws,
+                            size_t ws_bytes);
 
 /* ---- instrumentation ------------------------------------------------------------------------------ */
 /* For every timer whose bit is set in `mask`, each launch of that kernel family is bracketed by hipEvents

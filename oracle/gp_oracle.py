@@ -236,23 +236,25 @@ def kernel_grads(X: np.ndarray, p: KernelParams) -> dict:
 
 
 def mll_value_grad(X: np.ndarray, y: np.ndarray, p: KernelParams) -> dict:
-    """-log p(y) = 1/2 (y-m)^T alpha + sum log L_ii + n/2 log 2pi and its gradient
-    1/2 sum_ij (K^{-1} - alpha alpha^T)_ij dK_ij/d theta, d/dm = -sum alpha (the quantity
-    ExactMarginalLogLikelihood differentiates inside fit_gpytorch_mll [upstream], reached from
-    optimization/Bayesian.py:92-93, optimization/Bayesian6.py:480-488), before the 1/n scaling and priors."""
+    """-log p(Y) = sum_t [1/2 (y_t-m)^T alpha_t] + T (sum log L_ii + n/2 log 2pi) and its gradient
+    1/2 sum_ij (T K^{-1} - sum_t alpha_t alpha_t^T)_ij dK_ij/d theta, d/dm = -sum alpha, for T outputs sharing
+    the covariance (T = 1: the quantity ExactMarginalLogLikelihood differentiates inside fit_gpytorch_mll
+    [upstream], reached from optimization/Bayesian.py:92-93, optimization/Bayesian6.py:480-488), before the
+    1/n scaling and priors."""
     X = np.asarray(X, dtype=np.float64)
-    y = np.asarray(y, dtype=np.float64).reshape(-1)
-    n = X.shape[0]
-    st = fit(X, y, p)
+    Y = np.asarray(y, dtype=np.float64)
+    Y = Y.reshape(-1, 1) if Y.ndim == 1 else Y
+    n, T = Y.shape
+    st = fit(X, Y, p)
     L, alpha = st.L, st.alpha
-    quad = 0.5 * float((y - p.const_mean) @ alpha)
+    quad = 0.5 * float(((Y - p.const_mean) * alpha).sum())
     logdet = 2.0 * float(np.log(np.diag(L)).sum())
     Kinv = sla.cho_solve((L, True), np.eye(n), check_finite=False)
-    G = 0.5 * (Kinv - np.outer(alpha, alpha))
+    G = 0.5 * (T * Kinv - alpha @ alpha.T)
     dk = kernel_grads(X, p)
     d = X.shape[1]
     res = {
-        "nll": quad + 0.5 * logdet + 0.5 * n * math.log(2.0 * math.pi),
+        "nll": quad + T * (0.5 * logdet + 0.5 * n * math.log(2.0 * math.pi)),
         "quad": quad,
         "logdet": logdet,
         "noise": float(np.trace(G)),

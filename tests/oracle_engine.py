@@ -51,6 +51,18 @@ class OracleEngine:
             raise NotPositiveDefiniteError(e.pivot)
         return OState(st, torch.tensor(st.alpha.reshape(X.shape[0], -1)), X.shape[0], Y.shape[1], params)
 
+    def mll_value_grad(self, X, Y, params, jitters=(0.0, 1e-8, 1e-7, 1e-6), state=None):
+        self.calls["mll"] = self.calls.get("mll", 0) + 1
+        X = torch.as_tensor(X, dtype=torch.float64).cpu().numpy()
+        Y = torch.as_tensor(Y, dtype=torch.float64).cpu().numpy()
+        err = None
+        for jit in jitters:
+            try:
+                return O.mll_value_grad(X, Y, to_oracle_params(params.replace(jitter=params.jitter + jit), X.shape[1])), None
+            except O.NotPDError as e:
+                err = NotPositiveDefiniteError(e.pivot)
+        raise err
+
     def posterior(self, state, Xs, y_mean=None, y_scale=None):
         self.calls["posterior"] += 1
         Xs = torch.as_tensor(Xs, dtype=torch.float64).cpu().numpy()
