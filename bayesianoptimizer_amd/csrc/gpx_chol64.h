@@ -1,24 +1,18 @@
-// Factor + invert one 64x64 SPD diagonal block inside a 256-thread workgroup (used by potrf's panel kernel).
+// In-wave building blocks of the blocked Cholesky (gpx_potrf.hip): a 16x16 pivot block factored and inverted by
+// ONE wave in registers (no barrier per pivot), plus the 16x16 fp64-MFMA block products the panel kernel builds on.
 //
-// The serial part of a Cholesky is its pivot chain, so this routine keeps every pivot inside ONE wave with no
-// barrier and hands everything else to fp64 MFMA:
-//   for each 16-column step s = 0..3:
-//     F  (wave 0: lane r + 16 g owns row r, columns 4g..4g+3 of the 16x16 diagonal sub-block, fully unrolled):
-//          16 pivots, column/row broadcasts through LDS inside the wave -> L_ss and D_ss = L_ss^{-1}
-//     T  (3 waves): L_is = A_is D_ss^T for the sub-blocks below (16x16x16 MFMA from LDS)
-//     U  (4 waves): A_ij -= L_is L_js^T for the trailing sub-blocks (MFMA)
-//   then X = L^{-1} for the whole 64x64 by block forward substitution (X_ij = -D_ii sum_k L_ik X_kj, MFMA).
-// 3 barriers per step + 6 for the inverse, instead of 2 per pivot.
-//
-// LDS: sA (64 x LD64) holds A on entry and L (lower; strict upper set to 0) on exit; sX (64 x LD64) receives
-// L^{-1} (lower, strict upper 0); sT is a 64 x LD64 scratch.  Returns (in every thread) the 0-based failing
-// pivot, or -1.
+// Register layout of a 16x16 block in a wave: lane = r + 16 g owns row r, columns 4g..4g+3.  At pivot j the pivot
+// A[j][j] is one lane's register (v_readlane, uniform); every lane applies the unscaled rank-1 update
+// A[r][c] -= A[r][j] A[j][c] / A[j][j] and the same row operation on X = L^{-1}, with the cross-lane operands moved
+// by DPP and ds_bpermute, so only the pivot's rsq sits between two consecutive pivots.  LDS tiles use a padded row
+// length LD64 (doubles).
 #pragma once
+#include <utility>
 #include "gpx_device.h"
 
 namespace gpx {
 
-constexpr int LD64 = 68;  // padded row length (doubles) of the 64x64 LDS tiles
+constexpr int LD64 = 68;  // padded row length (doubles) of the 64-wide LDS tiles
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const unsigned long long u = __double_as_longlong(v);
@@ -27,9 +21,140 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
-// One 16x16 MFMA block product accumulated over K = 16*kb sub-blocks, operands from LDS tiles with row length
-// LD64: acc += sum_t A(ra0.., ka0 + t) * B(kb0 + t, cb0..) where A is read row-major (A[row][k]) and B is read
-// either row-major (B[k][col], BT=false) or as B[col][k] (BT=true, i.e. multiply by a transpose).
+// Lane J of every 16-lane row, broadcast to the whole row (v_mov_b64_dpp row_newbcast:J).
+template <int J>
+__device__ __forceinline__ double row_newbcast(double v) {
+  return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + J, 0xf, 0xf, false);
+}
+
+// Pivot reciprocal square root: v_rsq_f64 refined by one Newton step (~1 ulp; the correctly rounded sqrt +
+// division sequence costs ~25 dependent instructions on the pivot chain).
+__device__ __forceinline__ double pivot_rsq(double piv) {
+  double y = __builtin_amdgcn_rsq(piv);
+  const double h = 0.5 * piv;
+  const double e = fma(-h * y, y, 0.5);
+  return fma(y, e, y);
+}
+
+struct Blk16 {
+  double a[4];  // A: trailing rows updated in place; a row becomes scratch once it has been pivoted
+  double x[4];  // X = L^{-1} (the factorisation's row operations applied to I)
+  double l[4];  // L, captured column by column
+};
+
+// Lane J of every 16-lane row, broadcast to the whole row, as two v_mov_b32_dpp row_newbcast:J (no old value;
+// the 64-bit v_mov_b64_dpp form costs an extra zeroing move and a hazard nop per value, 17 cycles per link).
+template <int J>
+__device__ __forceinline__ double row_bcast(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(u & 0xffffffffull), 0x150 + J, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), 0x150 + J, 0xf, 0xf, false);
+  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// Value of lane `src_lane` (any lane of the wave), as a double: two ds_bpermute_b32 (LDS crossbar, no bank access).
+__device__ __forceinline__ double bpermute_f64(int src_lane, double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(u & 0xffffffffull));
+  const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(u >> 32));
+  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// Pivot J of the 16x16 block: rows r > J get A[r][c] -= A[r][J] A[J][c] / A[J][J], row J of X is scaled by
+// A[J][J]^{-1/2} and X's rows r > J get the same row operation; rows < J are left untouched.  Row J of A and of X
+// (the lane's own four columns) come from lane J of the same 16-lane DPP row (row_newbcast:J); A[r][J] lives in DPP
+// row J/4 and comes by ds_bpermute.  Measured per pivot: 306 cycles with 64-bit DPP moves, 390 with a wave-local
+// LDS broadcast slot (two ds_read_b128 per row, a write -> read round trip on the chain).
+template <int J>
+__device__ __forceinline__ void chol16_pivot(Blk16& b, int r, int g, int& fail) {
+  constexpr int GJ = J >> 2, QJ = J & 3;
+  const double piv = readlane_f64(b.a[QJ], J + 16 * GJ);
+  const double arj = bpermute_f64(r + 16 * GJ, b.a[QJ]);  // A[r][J]
+  double aj[4], xj[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    aj[q] = row_bcast<J>(b.a[q]);
+    xj[q] = row_bcast<J>(b.x[q]);
+  }
+  if (!(piv > 0.0) && fail < 0) fail = J;
+  const double isq = pivot_rsq(piv);
+  const double rinv = isq * isq;
+  const double coef = (r > J) ? -arj * rinv : 0.0;
+  const double coefx = (r == J) ? isq - 1.0 : coef;
+  if (g == GJ) b.l[QJ] = (r >= J) ? b.a[QJ] * isq : 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    b.a[q] = fma(coef, aj[q], b.a[q]);
+    b.x[q] = fma(coefx, xj[q], b.x[q]);
+  }
+}
+
+template <int... J>
+__device__ __forceinline__ void chol16_pivots(Blk16& b, int r, int g, int& fail, std::integer_sequence<int, J...>) {
+  (chol16_pivot<J>(b, r, g, fail), ...);
+}
+
+// Factor + invert the 16x16 SPD block at (o, o) of the LDS tile sA (both triangles present, symmetric) with one
+// wave: L (strict upper zeroed) back into sA, D = L^{-1} (lower, strict upper 0) into rows 0..15 / columns 0..15 of
+// sD.  Returns the 0-based failing pivot inside the block, or -1 (uniform).
+__device__ __forceinline__ int chol16(double* sA, double* sD, int o) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  Blk16 b;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    b.a[q] = sA[(o + r) * LD64 + o + 4 * g + q];
+    b.x[q] = (r == 4 * g + q) ? 1.0 : 0.0;
+    b.l[q] = 0.0;
+  }
+  int fail = -1;
+  chol16_pivots(b, r, g, fail, std::make_integer_sequence<int, 16>{});
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = 4 * g + q;
+    sA[(o + r) * LD64 + o + c] = b.l[q];
+    sD[r * LD64 + c] = (c <= r) ? b.x[q] : 0.0;
+  }
+  return fail;
+}
+
+// X = L^{-1} of the lower-triangular 16x16 block at (o, o) of sL (already factored), by one wave: forward
+// elimination on I with the rows of X broadcast by DPP and the multipliers read from LDS.  Written to sX at (o, o).
+template <int J>
+__device__ __forceinline__ void trinv16_step(double (&x)[4], const double (&lr)[16], double djinv, int r) {
+  double xj[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) xj[q] = row_newbcast<J>(x[q]) * djinv;
+  const double c = (r > J) ? lr[J] : 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) x[q] = (r == J) ? xj[q] : fma(-c, xj[q], x[q]);
+}
+
+template <int... J>
+__device__ __forceinline__ void trinv16_steps(double (&x)[4], const double (&lr)[16], const double (&dinv)[16], int r,
+                                              std::integer_sequence<int, J...>) {
+  (trinv16_step<J>(x, lr, dinv[J], r), ...);
+}
+
+__device__ __forceinline__ void trinv16_dpp(const double* sL, double* sX, int o) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  double lr[16], dinv[16], x[4];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    lr[j] = sL[(o + r) * LD64 + o + j];
+    dinv[j] = 1.0 / sL[(o + j) * LD64 + o + j];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) x[q] = (r == 4 * g + q) ? 1.0 : 0.0;
+  trinv16_steps(x, lr, dinv, r, std::make_integer_sequence<int, 16>{});
+#pragma unroll
+  for (int q = 0; q < 4; ++q) sX[(o + r) * LD64 + o + 4 * g + q] = x[q];
+}
+
+// One 16x16 MFMA block product accumulated over K: acc += sign * sum_t A(ra0 + m, ka0 + t) B(kb0 + t, cb0 + n)
+// with both operands in LDS tiles of row length LD64; A is read row-major (A[row][k]) and B either row-major
+// (B[k][col], BT=false) or as B[col][k] (BT=true, a multiply by a transpose).
 template <bool BT>
 __device__ __forceinline__ d4 mfma_lds16(d4 acc, const double* A, int ra0, int ka0, const double* B, int kb0, int cb0,
                                          int K, double sign) {
@@ -58,122 +183,19 @@ __device__ __forceinline__ void store_block16(double* S, int r0, int c0, d4 v) {
   for (int q = 0; q < 4; ++q) S[(r0 + (lane >> 4) + 4 * q) * LD64 + c0 + (lane & 15)] = v[q];
 }
 
-// Pivot square root and reciprocal: v_rsq_f64 refined by one Newton step (~1 ulp; the correctly rounded
-// sqrt + division sequences cost ~25 dependent instructions on the pivot chain).
-__device__ __forceinline__ void pivot_rsq(double piv, double& d, double& inv) {
-  double y = __builtin_amdgcn_rsq(piv);
-  const double h = 0.5 * piv;
-  const double e = fma(-h * y, y, 0.5);
-  y = fma(y, e, y);
-  inv = y;
-  d = piv * y;
-}
-
-// F phase: factor + invert the 16x16 block at (o, o) of sA with one whole wave; lane = r + 16 g owns row r,
-// columns 4g..4g+3 of A (a[]) and of X = L^{-1} (x[], built in the same right-looking sweep).  Each pivot
-// broadcasts column j of L and row j of X through two 16-double LDS slots (bc); LDS requests of one wave are
-// served in order, so no barrier is needed.  L goes to sA (strict upper zeroed), X to sX.
-__device__ __forceinline__ int chol16_wave(double* sA, double* sX, double* bc, int o) {
-  const int lane = threadIdx.x & 63;
-  const int r = lane & 15, g = lane >> 4;
-  double a[4], x[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    a[q] = sA[(o + r) * LD64 + o + 4 * g + q];
-    x[q] = (r == 4 * g + q) ? 1.0 : 0.0;
-  }
-  double* colbuf = bc;
-  double* rowbuf = bc + 16;
-  int fail = -1;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int gj = j >> 2, qj = j & 3;
-    const double piv = readlane_f64(a[qj], j + 16 * gj);
-    if (!(piv > 0.0) && fail < 0) fail = j;
-    double d, inv;
-    pivot_rsq(piv, d, inv);
-    if (g == gj) {
-      const double l = (r > j) ? a[qj] * inv : ((r == j) ? d : 0.0);
-      a[qj] = l;
-      colbuf[r] = l;
-    }
-    if (r == j) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        x[q] *= inv;
-        rowbuf[4 * g + q] = x[q];
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    const double lr = colbuf[r];
-    double lc[4], xj[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      lc[q] = colbuf[4 * g + q];
-      xj[q] = rowbuf[4 * g + q];
-    }
-    __builtin_amdgcn_wave_barrier();
-    if (r > j) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (4 * g + q > j) a[q] -= lr * lc[q];
-        x[q] -= lr * xj[q];
-      }
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int c = 4 * g + q;
-    sA[(o + r) * LD64 + o + c] = (c <= r) ? a[q] : 0.0;
-    sX[(o + r) * LD64 + o + c] = x[q];
-  }
-  return fail;
-}
-
-__device__ inline int chol_inv64(double* sA, double* sX, double* sT) {
+// Inverse of a 64x64 lower-triangular L held in sL (strict upper arbitrary) into sX (lower, strict upper zero),
+// 256 threads: each wave inverts one 16x16 diagonal block (trinv16_dpp), then X_ij = -X_ii sum_{k=j}^{i-1} L_ik X_kj
+// by sub-diagonal on MFMA (sT: 64 x LD64 scratch).
+__device__ inline void trinv64(const double* sL, double* sX, double* sT) {
   const int w = threadIdx.x >> 6;
-  __shared__ int s_fail;
-  if (threadIdx.x == 0) s_fail = -1;
-  for (int s = 0; s < 4; ++s) {
-    const int o = 16 * s;
-    if (w == 0) {
-      const int f = chol16_wave(sA, sX, sT, o);
-      if ((threadIdx.x & 63) == 0 && f >= 0 && s_fail < 0) s_fail = o + f;
-    }
-    __syncthreads();
-    // T: L_is = A_is D_ss^T (i = s+1..3), one sub-block per wave, written back in place (no other wave
-    // touches block (i, s) in this phase)
-    {
-      const int i = s + 1 + w;
-      if (i < 4) {
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
-        acc = mfma_lds16<true>(acc, sA, 16 * i, o, sX, o, o, 16, 1.0);  // B(k,n) = D[n][k]
-        store_block16(sA, 16 * i, o, acc);
-      }
-    }
-    __syncthreads();
-    // U: A_ij -= L_is L_js^T for s < j <= i <= 3
-    for (int e = w; e < 6; e += 4) {
-      // enumerate the lower sub-blocks of the 3x3 trailing grid
-      int ii, jj;
-      if (e == 0) { ii = 1; jj = 1; } else if (e == 1) { ii = 2; jj = 1; } else if (e == 2) { ii = 2; jj = 2; }
-      else if (e == 3) { ii = 3; jj = 1; } else if (e == 4) { ii = 3; jj = 2; } else { ii = 3; jj = 3; }
-      const int i = s + ii, j = s + jj;
-      if (i < 4 && j < 4) {
-        d4 acc = load_block16(sA, 16 * i, 16 * j);
-        acc = mfma_lds16<true>(acc, sA, 16 * i, o, sA, o, 16 * j, 16, -1.0);  // B(k,n) = L[j][k]
-        store_block16(sA, 16 * i, 16 * j, acc);
-      }
-    }
-    __syncthreads();
-  }
-  // X = L^{-1}: X_ii = D_ii (already in sX); X_ij = -D_ii * sum_{k=j}^{i-1} L_ik X_kj, by sub-diagonal.
+  trinv16_dpp(sL, sX, 16 * w);
+  __syncthreads();
   for (int dd = 1; dd < 4; ++dd) {
-    const int nb = 4 - dd;  // blocks on this sub-diagonal
+    const int nb = 4 - dd;
     if (w < nb) {
       const int j = w, i = w + dd;
       d4 acc = {0.0, 0.0, 0.0, 0.0};
-      for (int k = j; k < i; ++k) acc = mfma_lds16<false>(acc, sA, 16 * i, 16 * k, sX, 16 * k, 16 * j, 16, 1.0);
+      for (int k = j; k < i; ++k) acc = mfma_lds16<false>(acc, sL, 16 * i, 16 * k, sX, 16 * k, 16 * j, 16, 1.0);
       store_block16(sT, 16 * i, 16 * j, acc);
     }
     __syncthreads();
@@ -185,13 +207,11 @@ __device__ inline int chol_inv64(double* sA, double* sX, double* sT) {
     }
     __syncthreads();
   }
-  // zero the strict upper 16x16 blocks of X
   for (int e = threadIdx.x; e < 64 * 64; e += WG) {
     const int rr = e >> 6, cc = e & 63;
     if ((cc >> 4) > (rr >> 4)) sX[rr * LD64 + cc] = 0.0;
   }
   __syncthreads();
-  return s_fail;
 }
 
 }  // namespace gpx

@@ -1,4 +1,8 @@
-// Microbenchmark of the Cholesky panel / syrk kernels (diagnostic).  Includes the shipped kernels directly.
+// Microbenchmark + self-check of the blocked Cholesky kernels (diagnostic; includes the shipped gpx_potrf.hip).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form=1 -I../bayesianoptimizer_amd/csrc
+//        potrf_bench.hip -o potrf_bench_probe
+// Prints: the permlane/DPP broadcast semantics the in-wave pivot relies on, per-kernel times (panel with 1 and 64
+// workgroups, syrk at step 0, diagonal inverses, full potrf) and max |L L^T - A| / max |D L_kk - I| on the host.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -6,246 +10,142 @@
 #include <algorithm>
 #include <cmath>
 #include "gpx_internal.h"
+__device__ unsigned long long g_stamp[4][16];
+__device__ unsigned g_hwid[4];
+// wave-0 lane-0 timestamps of the panel phases, per wave w (lane 0): g_stamp[w][i]
+#define GPX_PANEL_STAMP(i) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 1) { g_stamp[threadIdx.x >> 6][i] = __builtin_readcyclecounter(); if (i == 0) g_hwid[threadIdx.x >> 6] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)); } } while (0)
 namespace gpx {  // timers are no-ops in this harness
 LaunchTimer::LaunchTimer(Context* ctx, int t) : c(ctx), timer(t) {}
 LaunchTimer::~LaunchTimer() {}
-}
+}  // namespace gpx
 #include "gpx_potrf.hip"
-namespace gpx {
-__global__ void __launch_bounds__(WG) old_panel_kernel(double* __restrict__ A, int64_t lda, int k,
-                                                         double* __restrict__ Dinv, int32_t* __restrict__ info) {
-  if (*(volatile int32_t*)info != 0) return;  // an earlier step failed: leave the rest untouched
-  __shared__ double colbuf[NB];
-  __shared__ double rowbuf[NB];
-  __shared__ double pivot;
-  __shared__ double sP[NB][NB + 1];   // panel block A_ik
-  __shared__ double sD[NB][NB + 1];   // D_k
 
-  const int t = threadIdx.x;
-  const int tr = t >> 4, tc = t & 15;  // owns rows 4tr..4tr+3, cols 4tc..4tc+3
-  const int bi = k + blockIdx.x;       // block row of this workgroup
-  const double* Akk = A + (int64_t)k * NB * lda + (int64_t)k * NB;
-
-  double a[4][4], x[4][4];
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const double4 v = *reinterpret_cast<const double4*>(Akk + (int64_t)(4 * tr + rr) * lda + 4 * tc);
-    a[rr][0] = v.x; a[rr][1] = v.y; a[rr][2] = v.z; a[rr][3] = v.w;
-#pragma unroll
-    for (int cc = 0; cc < 4; ++cc) x[rr][cc] = (4 * tr + rr == 4 * tc + cc) ? 1.0 : 0.0;
-  }
-  // Panel block load overlaps the factorisation.
-  if (blockIdx.x > 0) {
-    const double* Aik = A + (int64_t)bi * NB * lda + (int64_t)k * NB;
-    for (int e = t; e < NB * NB / 2; e += WG) {
-      int r = e / (NB / 2), c2 = (e % (NB / 2)) * 2;
-      const double2 v = *reinterpret_cast<const double2*>(Aik + (int64_t)r * lda + c2);
-      sP[r][c2] = v.x;
-      sP[r][c2 + 1] = v.y;
-    }
-  }
-  bool failed_reported = false;
-
-  for (int jb = 0; jb < NB / 4; ++jb) {
-#pragma unroll
-    for (int jr = 0; jr < 4; ++jr) {
-      const int j = 4 * jb + jr;
-      if (tr == jb && tc == jb) pivot = a[jr][jr];
-      __syncthreads();
-      const double pv = pivot;
-      const double dj = sqrt(pv);
-      const double inv_dj = 1.0 / dj;
-      if (!(pv > 0.0) && t == 0 && blockIdx.x == 0 && !failed_reported) {
-        atomicCAS(info, 0, k * NB + j + 1);
-        failed_reported = true;
-      }
-      if (tc == jb) {  // owners of column j publish L(:, j)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int row = 4 * tr + rr;
-          double l;
-          if (row > j) l = a[rr][jr] * inv_dj;
-          else if (row == j) l = dj;
-          else l = 0.0;
-          a[rr][jr] = l;
-          colbuf[row] = l;
-        }
-      }
-      if (tr == jb) {  // owners of row j of the inverse finalise and publish it
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-          x[jr][cc] *= inv_dj;
-          rowbuf[4 * tc + cc] = x[jr][cc];
-        }
-      }
-      __syncthreads();
-      double lr[4], lc[4], xr[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        lr[q] = colbuf[4 * tr + q];
-        lc[q] = colbuf[4 * tc + q];
-        xr[q] = rowbuf[4 * tc + q];
-      }
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int row = 4 * tr + rr;
-        if (row > j) {
-#pragma unroll
-          for (int cc = 0; cc < 4; ++cc) {
-            const int col = 4 * tc + cc;
-            if (col > j && col <= row) a[rr][cc] -= lr[rr] * lc[cc];
-            x[rr][cc] -= lr[rr] * xr[cc];
-          }
-        }
-      }
-    }
-  }
-
-  if (blockIdx.x == 0) {
-    const int nblk = gridDim.x + k;
-    double* D = Dinv + (int64_t)k * NB * NB;
-    double* Lkk = Dinv + (int64_t)(nblk + k) * NB * NB;  // scratch copy, moved into A by syrk_update
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int row = 4 * tr + rr;
-      double4 lv, dv;
-      lv.x = (4 * tc + 0 <= row) ? a[rr][0] : 0.0;
-      lv.y = (4 * tc + 1 <= row) ? a[rr][1] : 0.0;
-      lv.z = (4 * tc + 2 <= row) ? a[rr][2] : 0.0;
-      lv.w = (4 * tc + 3 <= row) ? a[rr][3] : 0.0;
-      dv.x = x[rr][0]; dv.y = x[rr][1]; dv.z = x[rr][2]; dv.w = x[rr][3];
-      *reinterpret_cast<double4*>(Lkk + row * NB + 4 * tc) = lv;
-      *reinterpret_cast<double4*>(D + row * NB + 4 * tc) = dv;
-    }
-    return;
-  }
-  // Panel: L_ik[r][c] = sum_q A_ik[r][q] * D[c][q]  (D lower triangular: q <= c)
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr)
-#pragma unroll
-    for (int cc = 0; cc < 4; ++cc) sD[4 * tr + rr][4 * tc + cc] = x[rr][cc];
-  __syncthreads();
-  double acc[4][4];
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr)
-#pragma unroll
-    for (int cc = 0; cc < 4; ++cc) acc[rr][cc] = 0.0;
-  const int qmax = 4 * tc + 4;
-  for (int q = 0; q < qmax; ++q) {
-    double av[4], dv[4];
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) av[rr] = sP[4 * tr + rr][q];
-#pragma unroll
-    for (int cc = 0; cc < 4; ++cc) dv[cc] = sD[4 * tc + cc][q];
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr)
-#pragma unroll
-      for (int cc = 0; cc < 4; ++cc) acc[rr][cc] += av[rr] * dv[cc];
-  }
-  double* Lik = A + (int64_t)bi * NB * lda + (int64_t)k * NB;
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    double4 v;
-    v.x = acc[rr][0]; v.y = acc[rr][1]; v.z = acc[rr][2]; v.w = acc[rr][3];
-    *reinterpret_cast<double4*>(Lik + (int64_t)(4 * tr + rr) * lda + 4 * tc) = v;
-  }
-}
-
-}
-
-namespace gpx {
-__device__ unsigned long long g_stamp[64];
-__device__ __forceinline__ void stamp(int i) {
-  __builtin_amdgcn_sched_barrier(0);
-  unsigned long long t = __builtin_amdgcn_s_memtime();
-  if (threadIdx.x == 0) g_stamp[i] = t;
-  __builtin_amdgcn_sched_barrier(0);
-}
-__global__ void __launch_bounds__(WG) stamped_chol(const double* A, int64_t lda) {
-  __shared__ __attribute__((aligned(16))) double sA[NB * LD64];
-  __shared__ __attribute__((aligned(16))) double sX[NB * LD64];
-  __shared__ __attribute__((aligned(16))) double sT[NB * LD64];
-  for (int e = threadIdx.x; e < 64 * 64; e += WG) sA[(e >> 6) * LD64 + (e & 63)] = A[(e >> 6) * lda + (e & 63)];
-  __syncthreads();
-  stamp(0);
-  const int w = threadIdx.x >> 6;
-  for (int s = 0; s < 4; ++s) {
-    const int o = 16 * s;
-    if (w == 0) chol16_wave(sA, sX, sT, o);
-    __syncthreads();
-    stamp(1 + 3 * s);
-    { const int i = s + 1 + w; if (i < 4) { d4 acc = {0,0,0,0}; acc = mfma_lds16<true>(acc, sA, 16*i, o, sX, o, o, 16, 1.0); store_block16(sA, 16*i, o, acc);} }
-    __syncthreads();
-    stamp(2 + 3 * s);
-    for (int e = w; e < 6; e += 4) {
-      int ii, jj;
-      if (e == 0) { ii = 1; jj = 1; } else if (e == 1) { ii = 2; jj = 1; } else if (e == 2) { ii = 2; jj = 2; }
-      else if (e == 3) { ii = 3; jj = 1; } else if (e == 4) { ii = 3; jj = 2; } else { ii = 3; jj = 3; }
-      const int i = s + ii, j = s + jj;
-      if (i < 4 && j < 4) { d4 acc = load_block16(sA, 16*i, 16*j); acc = mfma_lds16<true>(acc, sA, 16*i, o, sA, o, 16*j, 16, -1.0); store_block16(sA, 16*i, 16*j, acc); }
-    }
-    __syncthreads();
-    stamp(3 + 3 * s);
-  }
-}
-}
 using namespace gpx;
-#define CK(x) do{hipError_t e=(x); if(e!=hipSuccess){printf("HIP error %s at %d\n",hipGetErrorString(e),__LINE__); exit(1);}}while(0)
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
-int main() {
-  const int n = 4096, nblk = n / 64;
-  std::vector<double> h((size_t)n * n);
-  srand(3);
-  // SPD: exp(-|i-j|/200)-like smooth matrix + diag
-  for (int i = 0; i < n; ++i) for (int j = 0; j < n; ++j) h[(size_t)i*n+j] = exp(-fabs(i-j)/300.0) + (i==j ? 1e-2 : 0.0);
+__global__ void bcast_probe(double* out) {
+  const int l = threadIdx.x;
+  const double v = 100.0 * (l >> 4) + (l & 15);
+  out[l] = row_newbcast<5>(v);
+}
+
+__global__ void f16_test(const double* A, double* L, double* X, int* fail) {
+  __shared__ double sA[16 * LD64], sD[16 * LD64];
+
+  for (int e = threadIdx.x; e < 256; e += 64) sA[(e >> 4) * LD64 + (e & 15)] = A[e];
+  __syncthreads();
+  const int f = chol16(sA, sD, 0);
+  __syncthreads();
+  for (int e = threadIdx.x; e < 256; e += 64) { L[e] = sA[(e >> 4) * LD64 + (e & 15)]; X[e] = sD[(e >> 4) * LD64 + (e & 15)]; }
+  if (threadIdx.x == 0) *fail = f;
+}
+
+int main(int argc, char** argv) {
+  {
+    std::vector<double> a(256), l(256), x(256);
+    for (int i = 0; i < 16; ++i) for (int j = 0; j < 16; ++j) a[i * 16 + j] = exp(-0.05 * (i - j) * (i - j)) + (i == j ? 0.1 : 0.0);
+    double *dA, *dL, *dX; int* df;
+    CK(hipMalloc(&dA, 2048)); CK(hipMalloc(&dL, 2048)); CK(hipMalloc(&dX, 2048)); CK(hipMalloc(&df, 4));
+    CK(hipMemcpy(dA, a.data(), 2048, hipMemcpyHostToDevice));
+    f16_test<<<1, 64>>>(dA, dL, dX, df);
+    int f; CK(hipMemcpy(l.data(), dL, 2048, hipMemcpyDeviceToHost)); CK(hipMemcpy(x.data(), dX, 2048, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(&f, df, 4, hipMemcpyDeviceToHost));
+    std::vector<double> ref(256, 0.0);
+    for (int j = 0; j < 16; ++j) {
+      double s = a[j * 16 + j]; for (int k = 0; k < j; ++k) s -= ref[j * 16 + k] * ref[j * 16 + k];
+      ref[j * 16 + j] = sqrt(s);
+      for (int i = j + 1; i < 16; ++i) { double t = a[i * 16 + j]; for (int k = 0; k < j; ++k) t -= ref[i * 16 + k] * ref[j * 16 + k]; ref[i * 16 + j] = t / ref[j * 16 + j]; }
+    }
+    double el = 0, ex = 0;
+    for (int i = 0; i < 16; ++i) for (int j = 0; j < 16; ++j) {
+      el = std::max(el, fabs(l[i * 16 + j] - ref[i * 16 + j]));
+      double s = 0; for (int k = 0; k < 16; ++k) s += x[i * 16 + k] * ref[k * 16 + j];
+      ex = std::max(ex, fabs(s - (i == j)));
+    }
+    printf("chol16: fail=%d max|L-Lref|=%.3e max|X L - I|=%.3e\n", f, el, ex);
+    if (el > 1e-12) { for (int i = 0; i < 4; ++i) { for (int j = 0; j < 6; ++j) printf(" %9.5f/%9.5f", l[i*16+j], ref[i*16+j]); printf("\n"); } }
+  }
+  const int n = argc > 1 ? atoi(argv[1]) : 4096, nblk = n / 64;
+  {
+    double* d; CK(hipMalloc(&d, 192 * 8));
+    bcast_probe<<<1, 64>>>(d);
+    std::vector<double> h(192); CK(hipMemcpy(h.data(), d, 192 * 8, hipMemcpyDeviceToHost));
+    int bad = 0;
+    for (int l = 0; l < 64; ++l) {
+      bad += h[l] != 100.0 * (l >> 4) + 5;
+    }
+    printf("broadcast probe: %s (newbcast:5 lane 33: %.0f)\n", bad ? "MISMATCH" : "ok", h[33]);
+    CK(hipFree(d));
+  }
+  // SPD test matrix: RBF Gram of seeded points in [0,1]^8 (lengthscale 0.579) + 1e-4 I, like the bench problem
+  std::vector<double> h((size_t)n * n), X((size_t)n * 8);
+  srand(7);
+  for (auto& v : X) v = rand() / (double)RAND_MAX;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      double r2 = 0.0;
+      for (int k = 0; k < 8; ++k) { const double d = (X[i * 8 + k] - X[j * 8 + k]) / 0.579; r2 += d * d; }
+      h[(size_t)i * n + j] = exp(-0.5 * r2) + (i == j ? 1e-4 : 0.0);
+    }
   double *A, *A0, *Dinv; int* info;
-  CK(hipMalloc(&A, (size_t)n*n*8)); CK(hipMalloc(&A0, (size_t)n*n*8)); CK(hipMalloc(&Dinv, (size_t)2*nblk*64*64*8)); CK(hipMalloc(&info, 4));
-  CK(hipMemcpy(A0, h.data(), h.size()*8, hipMemcpyHostToDevice));
-  CK(hipMemset(info, 0, 4));
+  CK(hipMalloc(&A, (size_t)n * n * 8)); CK(hipMalloc(&A0, (size_t)n * n * 8));
+  CK(hipMalloc(&Dinv, (size_t)2 * nblk * 64 * 64 * 8)); CK(hipMalloc(&info, 4));
+  CK(hipMemcpy(A0, h.data(), h.size() * 8, hipMemcpyHostToDevice));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   auto timeit = [&](auto fn, int reps) {
     std::vector<float> t;
     for (int r = 0; r < reps; ++r) {
-      CK(hipMemcpy(A, A0, (size_t)n*n*8, hipMemcpyDeviceToDevice));
+      CK(hipMemcpy(A, A0, (size_t)n * n * 8, hipMemcpyDeviceToDevice));
       CK(hipMemset(info, 0, 4));
       CK(hipDeviceSynchronize());
       CK(hipEventRecord(e0)); fn(); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
       float ms; CK(hipEventElapsedTime(&ms, e0, e1)); t.push_back(ms);
     }
-    std::sort(t.begin(), t.end()); return t[t.size()/2];
+    std::sort(t.begin(), t.end()); return t[t.size() / 2];
   };
-  // correctness of the new panel vs the previous one on step 0
-  double *Dold; CK(hipMalloc(&Dold, (size_t)2*nblk*64*64*8));
-  double *Aold; CK(hipMalloc(&Aold, (size_t)n*n*8));
-  CK(hipMemcpy(Aold, A0, (size_t)n*n*8, hipMemcpyDeviceToDevice)); CK(hipMemcpy(A, A0, (size_t)n*n*8, hipMemcpyDeviceToDevice));
-  CK(hipMemset(info, 0, 4));
-  old_panel_kernel<<<nblk, WG>>>(Aold, n, 0, Dold, info);
-  potrf_panel_kernel<<<nblk, WG>>>(A, n, 0, Dinv, info);
-  CK(hipDeviceSynchronize());
-  {
-    std::vector<double> a((size_t)n*n), b((size_t)n*n), da(2*nblk*4096), db(2*nblk*4096);
-    CK(hipMemcpy(a.data(), Aold, a.size()*8, hipMemcpyDeviceToHost)); CK(hipMemcpy(b.data(), A, b.size()*8, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(da.data(), Dold, da.size()*8, hipMemcpyDeviceToHost)); CK(hipMemcpy(db.data(), Dinv, db.size()*8, hipMemcpyDeviceToHost));
-    double mp = 0, md = 0, ml = 0;
-    for (int i = 64; i < n; ++i) for (int j = 0; j < 64; ++j) mp = std::max(mp, fabs(a[(size_t)i*n+j]-b[(size_t)i*n+j]));
-    for (int e = 0; e < 4096; ++e) { md = std::max(md, fabs(da[e]-db[e])); ml = std::max(ml, fabs(da[nblk*4096+e]-db[nblk*4096+e])); }
-    printf("new vs old panel: max|dL_panel|=%.3e max|dD|=%.3e max|dL_kk|=%.3e\n", mp, md, ml);
-  }
-  float t1 = timeit([&]{ for (int i=0;i<10;++i) potrf_panel_kernel<<<1, WG>>>(A, n, 0, Dinv, info); }, 5);
-  float t1o = timeit([&]{ for (int i=0;i<10;++i) old_panel_kernel<<<1, WG>>>(A, n, 0, Dinv, info); }, 5);
-  printf("OLD panel kernel grid=1: %.2f us\n", t1o*100);
-  printf("panel kernel grid=1 (diag factor+inverse only): %.2f us\n", t1*100);
-  float t64 = timeit([&]{ for (int i=0;i<10;++i) potrf_panel_kernel<<<64, WG>>>(A, n, 0, Dinv, info); }, 5);
-  printf("panel kernel grid=64 (diag + 63 TRSM WGs): %.2f us\n", t64*100);
-  float ts = timeit([&]{ for (int i=0;i<10;++i) syrk_update_kernel<<<63*64/2+1, WG>>>(A, n, 0, nblk, Dinv, info); }, 5);
-  printf("syrk step 0 (2016 tiles): %.2f us\n", ts*100);
   Context c; c.stream = 0;
-  float tp = timeit([&]{ launch_potrf(&c, n, A, n, Dinv, info); }, 5);
-  printf("full potrf n=4096: %.3f ms\n", tp);
-  int hinfo; CK(hipMemcpy(&hinfo, info, 4, hipMemcpyDeviceToHost)); printf("info=%d\n", hinfo);
-  stamped_chol<<<1, WG>>>(A0, n); CK(hipDeviceSynchronize());
-  stamped_chol<<<1, WG>>>(A0, n); CK(hipDeviceSynchronize());
-  unsigned long long hs[64]; CK(hipMemcpyFromSymbol(hs, HIP_SYMBOL(g_stamp), sizeof(hs)));
-  for (int i = 1; i <= 12; ++i) printf("stamp %2d: +%llu cycles\n", i, hs[i] - hs[i-1]);
+  const float tp = timeit([&] { (void)launch_potrf(&c, n, A, n, Dinv, info); }, 7);
+  int hinfo; CK(hipMemcpy(&hinfo, info, 4, hipMemcpyDeviceToHost));
+  std::vector<double> L((size_t)n * n), D((size_t)nblk * 4096);
+  CK(hipMemcpy(L.data(), A, L.size() * 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(D.data(), Dinv, D.size() * 8, hipMemcpyDeviceToHost));
+  // residual on sampled rows
+  double res = 0.0;
+  for (int i = 0; i < n; i += 37) {
+    for (int j = 0; j <= i; ++j) {
+      double s = 0.0;
+      for (int k = 0; k <= j; ++k) s += L[(size_t)i * n + k] * L[(size_t)j * n + k];
+      res = std::max(res, fabs(s - h[(size_t)i * n + j]));
+    }
+  }
+  double dres = 0.0;
+  for (int b = 0; b < nblk; b += 7) {
+    for (int r = 0; r < 64; ++r) for (int cc = 0; cc < 64; ++cc) {
+      double s = 0.0;
+      for (int k = 0; k < 64; ++k) s += D[(size_t)b * 4096 + r * 64 + k] * L[(size_t)(64 * b + k) * n + 64 * b + cc];
+      dres = std::max(dres, fabs(s - (r == cc ? 1.0 : 0.0)));
+    }
+  }
+  printf("n=%d full potrf: %.3f ms  info=%d  max|LL^T-A| (sampled rows)=%.3e  max|D L_kk - I|=%.3e\n", n, tp, hinfo, res, dres);
+  const float t1 = timeit([&] { for (int i = 0; i < 20; ++i) potrf_panel_kernel<<<1, WG>>>(A, n, 0, Dinv, info); }, 5);
+  const float t64 = timeit([&] { for (int i = 0; i < 20; ++i) potrf_panel_kernel<<<nblk, WG>>>(A, n, 0, Dinv, info); }, 5);
+  const float ts = timeit([&] { for (int i = 0; i < 20; ++i) syrk_update_kernel<<<(nblk - 1) * nblk / 2 + 1, WG>>>(A, n, 0, nblk, Dinv, info); }, 5);
+  const float ts60 = timeit([&] { for (int i = 0; i < 20; ++i) syrk_update_kernel<<<4 * 3 / 2 + 1, WG>>>(A, n, nblk - 4, nblk, Dinv, info); }, 5);
+  const float td = timeit([&] { for (int i = 0; i < 20; ++i) potrf_dinv_kernel<<<nblk, WG>>>(A, n, Dinv, info); }, 5);
+  printf("panel grid=1: %.2f us   panel grid=%d: %.2f us   syrk step0 (%d tiles): %.2f us   syrk step %d: %.2f us   dinv: %.2f us\n",
+         t1 * 50, nblk, t64 * 50, (nblk - 1) * nblk / 2, ts * 50, nblk - 4, ts60 * 50, td * 50);
+  CK(hipMemcpy(A, A0, (size_t)n * n * 8, hipMemcpyDeviceToDevice)); CK(hipMemset(info, 0, 4));
+  potrf_panel_kernel<<<nblk, WG>>>(A, n, 0, Dinv, info); CK(hipDeviceSynchronize());
+  CK(hipMemcpy(A, A0, (size_t)n * n * 8, hipMemcpyDeviceToDevice)); CK(hipMemset(info, 0, 4));
+  potrf_panel_kernel<<<nblk, WG>>>(A, n, 0, Dinv, info); CK(hipDeviceSynchronize());
+  unsigned long long hs[4][16]; CK(hipMemcpyFromSymbol(hs, HIP_SYMBOL(g_stamp), sizeof(hs)));
+  unsigned hw[4]; CK(hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_hwid), sizeof(hw)));
+  for (int w = 0; w < 4; ++w) printf("wave %d HW_ID 0x%08x (simd %u, cu %u)\n", w, hw[w], (hw[w] >> 4) & 3, (hw[w] >> 8) & 15);
+  for (int w = 0; w < 4; ++w) {
+    printf("wave %d stamps (cycles after load):", w);
+    for (int i = 1; i <= 13; ++i) printf(" %lld", (long long)(hs[w][i] - hs[0][0]));
+    printf("\n");
+  }
   printf("POTRF BENCH DONE\n");
+  return 0;
 }
