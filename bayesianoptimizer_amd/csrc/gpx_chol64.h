@@ -95,8 +95,9 @@ __device__ __forceinline__ void chol16_pivots(Blk16& b, int r, int g, int& fail,
 }
 
 // Factor + invert the 16x16 SPD block at (o, o) of the LDS tile sA (both triangles present, symmetric) with one
-// wave: L (strict upper zeroed) back into sA, D = L^{-1} (lower, strict upper 0) into rows 0..15 / columns 0..15 of
-// sD.  Returns the 0-based failing pivot inside the block, or -1 (uniform).
+// wave: L (strict upper zeroed) back into sA, D = L^{-1} (lower, strict upper 0) into a 16x16 tile sD of row length
+// LDD.  Returns the 0-based failing pivot inside the block, or -1 (uniform).
+template <int LDD>
 __device__ __forceinline__ int chol16(double* sA, double* sD, int o) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
@@ -113,7 +114,7 @@ __device__ __forceinline__ int chol16(double* sA, double* sD, int o) {
   for (int q = 0; q < 4; ++q) {
     const int c = 4 * g + q;
     sA[(o + r) * LD64 + o + c] = b.l[q];
-    sD[r * LD64 + c] = (c <= r) ? b.x[q] : 0.0;
+    sD[r * LDD + c] = (c <= r) ? b.x[q] : 0.0;
   }
   return fail;
 }
@@ -153,9 +154,9 @@ __device__ __forceinline__ void trinv16_dpp(const double* sL, double* sX, int o)
 }
 
 // One 16x16 MFMA block product accumulated over K: acc += sign * sum_t A(ra0 + m, ka0 + t) B(kb0 + t, cb0 + n)
-// with both operands in LDS tiles of row length LD64; A is read row-major (A[row][k]) and B either row-major
+// with both operands in LDS tiles (row length LD64 for A, LDB for B); A is read row-major (A[row][k]) and B either row-major
 // (B[k][col], BT=false) or as B[col][k] (BT=true, a multiply by a transpose).
-template <bool BT>
+template <bool BT, int LDB = LD64>
 __device__ __forceinline__ d4 mfma_lds16(d4 acc, const double* A, int ra0, int ka0, const double* B, int kb0, int cb0,
                                          int K, double sign) {
   const int lane = threadIdx.x & 63;
@@ -163,7 +164,7 @@ __device__ __forceinline__ d4 mfma_lds16(d4 acc, const double* A, int ra0, int k
 #pragma unroll 4
   for (int k = 0; k < K; k += 4) {
     const double a = sign * A[(ra0 + m) * LD64 + ka0 + k + kk];
-    const double b = BT ? B[(cb0 + m) * LD64 + kb0 + k + kk] : B[(kb0 + k + kk) * LD64 + cb0 + m];
+    const double b = BT ? B[(cb0 + m) * LDB + kb0 + k + kk] : B[(kb0 + k + kk) * LDB + cb0 + m];
     acc = mfma16x16x4(a, b, acc);
   }
   return acc;

@@ -1,21 +1,27 @@
-// Blocked right-looking Cholesky (lower) of the padded Gram matrix, NB = 64.
+// Blocked right-looking Cholesky (lower) of the padded Gram matrix, NB = 64, ONE launch per block column.
 // SURVEY §8a row a4 — replaces psd_safe_cholesky in GPyTorch's exact path [upstream]; the reference's
 // jitter-retry policy (optimization/Bayesian6.py:481-488) needs the failing pivot, reported in *info.
 //
-// Per block column k, two launches:
-//  1. potrf_panel: one workgroup per block row i >= k factors the tall panel [A_kk; A_ik] (128 x 64, or just
-//     A_kk for i == k) in LDS: four 16-column steps, each
+// Launch c (c = 0 .. nblk-1) holds two independent kinds of workgroup:
+//  * panel workgroups p = 0 .. nblk-c-1 (row block i = c + p) factor block column c.  For c > 0 they first apply
+//    the step-(c-1) update to exactly the tiles they need, A_cc -= L_{c,c-1} L_{c,c-1}^T and
+//    A_ic -= L_{i,c-1} L_{c,c-1}^T (64x64x64 on fp64 MFMA, MfmaTile), then factor the tall panel [A_cc; A_ic]
+//    (128 x 64, or A_cc alone for p = 0) in LDS in four 16-column steps:
 //        F  wave 0 factors + inverts the 16x16 pivot block in registers (chol16, gpx_chol64.h),
 //        T  L_is = A_is D_ss^T for the 16-row blocks below it (fp64 MFMA),
 //        U  A_ij -= L_is L_js^T for the trailing 16x16 blocks of the panel (fp64 MFMA),
-//     with a one-block lookahead: wave 0 does the T and U of the next pivot block itself and goes straight on to
-//     the next F (one barrier per step); waves 1-3 do the other T items, wait on an LDS counter until every T item
-//     of the step is published, and do the other U items while that F runs.  Re-factoring A_kk in every workgroup
-//     costs no latency and needs no extra launch; workgroup i == k stores L_kk in the scratch half of Dinv
-//     (A_kk must stay intact while other workgroups may still read it), workgroups i > k store L_ik.
-//  2. syrk_update: trailing A_ij -= L_ik L_jk^T for all lower tiles i >= j > k on fp64 MFMA (MfmaTile);
-//     one extra workgroup copies L_kk from the scratch into A_kk.
-// Finally potrf_dinv inverts every 64x64 diagonal block of L in one launch (Dinv, used by gpx_trtri_f64).
+//    with a one-block lookahead: wave 0 does the T and U of the next pivot block itself and goes straight on to the
+//    next F (one barrier per step); waves 1-3 do the other T items, wait on an LDS counter until every T item of the
+//    step is published, and do the other U items while that F runs.  Every panel workgroup re-factors A_cc (no
+//    extra latency, no extra launch); p = 0 stores L_cc in the scratch half of Dinv (A_cc must stay intact while
+//    the other panel workgroups read it), p > 0 store L_ic.
+//  * trailing workgroups apply the step-(c-1) update to every lower tile of columns >= c+1:
+//    A_ij -= L_{i,c-1} L_{j,c-1}^T on 128x128 MfmaTiles (half the HBM/L2 traffic per flop of 64x64 tiles; the
+//    update is traffic-bound at 64x64: 36 us for the 2016 tiles of step 0).
+// Column c+1 is thus updated by step c-1 in launch c and by step c inside the panel workgroups of launch c+1, so
+// the panel factorisation (the latency-bound serial chain) overlaps the trailing update of the previous step
+// instead of following it.  potrf_dinv finally copies every L_kk from the scratch into A and inverts it (Dinv, used
+// by gpx_trtri_f64).
 #include "gpx_internal.h"
 #include "gpx_device.h"
 #include "gpx_chol64.h"
@@ -27,35 +33,76 @@
 
 namespace gpx {
 
-__global__ void __launch_bounds__(WG) potrf_panel_kernel(double* __restrict__ A, int64_t lda, int k,
-                                                         double* __restrict__ Dinv, int32_t* __restrict__ info) {
-  if (*(volatile int32_t*)info != 0) return;  // an earlier step failed: leave the rest untouched
-  __shared__ __attribute__((aligned(16))) double sA[NB * LD64];      // A_kk -> L_kk
-  __shared__ __attribute__((aligned(16))) double sP[NB * LD64];      // A_ik -> L_ik (i > k)
-  __shared__ __attribute__((aligned(16))) double sD[2][16 * LD64];   // D_ss, double-buffered by step parity
-  __shared__ int s_tdone;                                            // T items published (4 per step)
-  const int t = threadIdx.x, w = t >> 6;
-  const bool panel = blockIdx.x > 0;
-  const int nrow = panel ? 8 : 4;  // 16-row blocks of the tall panel
-  const int bi = k + blockIdx.x;
-  const double* Akk = A + (int64_t)k * NB * lda + (int64_t)k * NB;
-  double* Aik = A + (int64_t)bi * NB * lda + (int64_t)k * NB;
-  if (t == 0) s_tdone = 0;
+using Tile64 = MfmaTile<NB, NB, 16, false, false>;        // panel-side update (one 64x64 tile)
+using Tile128 = MfmaTile<2 * NB, 2 * NB, 16, false, false>;  // trailing update
+// LDS budget: two workgroups per CU (<= 80 KB each), so a trailing tile's loads and epilogue overlap another
+// tile's MFMAs (one 128x128x64 tile alone takes ~14 us; at one workgroup per CU step 1 took 43 us for 496 tiles).
+// Panel: sA, sP (64 x LD64 each) and the two D_ss buffers (16 x LDD); the Tile64 staging of the panel-side
+// update aliases sP + the D buffers (both written only after the update GEMMs).
+constexpr int LDD = 20;
+constexpr int DBUF = 768;  // >= 2 * 16 * LDD, sized so that sP + D buffers hold Tile64::LDS_DOUBLES
+static_assert(NB * LD64 + DBUF >= Tile64::LDS_DOUBLES && DBUF >= 2 * 16 * LDD, "panel LDS aliasing");
+constexpr int PANEL_LDS = 2 * NB * LD64 + DBUF;
+constexpr int STEP_LDS = PANEL_LDS > Tile128::LDS_DOUBLES ? PANEL_LDS : Tile128::LDS_DOUBLES;
+
+// C (64x64 at Cg, global) - acc  -> LDS tile S (row length LD64)
+__device__ __forceinline__ void tile_sub_to_lds(const Tile64& tl, const double* __restrict__ Cg, int64_t ldc, double* S) {
+  double cv[Tile64::WM][Tile64::WN][4];
+#pragma unroll
+  for (int i = 0; i < Tile64::WM; ++i)
+#pragma unroll
+    for (int j = 0; j < Tile64::WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cv[i][j][r] = Cg[(int64_t)Tile64::row_of(i, r) * ldc + Tile64::col_of(j)];
+#pragma unroll
+  for (int i = 0; i < Tile64::WM; ++i)
+#pragma unroll
+    for (int j = 0; j < Tile64::WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) S[Tile64::row_of(i, r) * LD64 + Tile64::col_of(j)] = cv[i][j][r] - tl.acc[i][j][r];
+}
+
+__device__ __forceinline__ void load_tile_lds(const double* __restrict__ G, int64_t ld, double* S) {
+  const int t = threadIdx.x;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int e = (t + q * WG) * 2, r = e >> 6, c = e & 63;
-    const double2 v = *reinterpret_cast<const double2*>(Akk + (int64_t)r * lda + c);
-    sA[r * LD64 + c] = v.x;
-    sA[r * LD64 + c + 1] = v.y;
+    const double2 v = *reinterpret_cast<const double2*>(G + (int64_t)r * ld + c);
+    S[r * LD64 + c] = v.x;
+    S[r * LD64 + c + 1] = v.y;
   }
-  if (panel) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int e = (t + q * WG) * 2, r = e >> 6, c = e & 63;
-      const double2 v = *reinterpret_cast<const double2*>(Aik + (int64_t)r * lda + c);
-      sP[r * LD64 + c] = v.x;
-      sP[r * LD64 + c + 1] = v.y;
+}
+
+// Panel workgroup p of block column c (see the file comment).
+__device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, int c, int p, int nblk,
+                                           double* __restrict__ Dinv, int32_t* __restrict__ info, double* lds) {
+  double* sA = lds;             // A_cc -> L_cc
+  double* sP = sA + NB * LD64;  // A_ic -> L_ic (p > 0)
+  double* sDb = sP + NB * LD64; // D_ss, double-buffered by step parity (2 x 16 x LDD)
+  double* smem = sP;            // Tile64 staging of the update GEMMs (aliases sP + sDb)
+  __shared__ int s_tdone;              // T items published (4 per step)
+  const int t = threadIdx.x, w = t >> 6;
+  const bool panel = p > 0;
+  const int nrow = panel ? 8 : 4;  // 16-row blocks of the tall panel
+  const int bi = c + p;
+  const double* Acc = A + (int64_t)c * NB * lda + (int64_t)c * NB;
+  double* Aic = A + (int64_t)bi * NB * lda + (int64_t)c * NB;
+  if (t == 0) s_tdone = 0;
+  if (c > 0) {
+    // step-(c-1) update of the two tiles this workgroup factors
+    const double* Lc = A + (int64_t)c * NB * lda + (int64_t)(c - 1) * NB;
+    Tile64 tl;
+    tl.run(Lc, lda, Lc, lda, 0, NB, smem);
+    tile_sub_to_lds(tl, Acc, lda, sA);
+    if (panel) {
+      __syncthreads();  // smem reuse
+      tl.run(A + (int64_t)bi * NB * lda + (int64_t)(c - 1) * NB, lda, Lc, lda, 0, NB, smem);
+      // run() ends with a barrier after its last LDS read, so the epilogue may overwrite the staging (sP)
+      tile_sub_to_lds(tl, Aic, lda, sP);
     }
+  } else {
+    load_tile_lds(Acc, lda, sA);
+    if (panel) load_tile_lds(Aic, lda, sP);
   }
   __syncthreads();
   GPX_PANEL_STAMP(0);
@@ -64,7 +111,7 @@ __global__ void __launch_bounds__(WG) potrf_panel_kernel(double* __restrict__ A,
   auto tsolve = [&](int i, const double* D, int o) {
     double* R = rows(i);
     d4 acc = {0.0, 0.0, 0.0, 0.0};
-    acc = mfma_lds16<true>(acc, R, 0, o, D, 0, 0, 16, 1.0);
+    acc = mfma_lds16<true, LDD>(acc, R, 0, o, D, 0, 0, 16, 1.0);
     store_block16(R, 0, o, acc);
   };
   // U: A_ij -= L_is L_js^T
@@ -81,9 +128,9 @@ __global__ void __launch_bounds__(WG) potrf_panel_kernel(double* __restrict__ A,
   int fail = -1;
   for (int s = 0; s < 4; ++s) {
     const int o = 16 * s;
-    double* D = sD[s & 1];
+    double* D = sDb + (s & 1) * 16 * LDD;
     if (w == 0) {
-      const int f = chol16(sA, D, o);
+      const int f = chol16<LDD>(sA, D, o);
       if (f >= 0 && fail < 0) fail = o + f;
     }
     GPX_PANEL_STAMP(1 + 3 * s);
@@ -116,79 +163,84 @@ __global__ void __launch_bounds__(WG) potrf_panel_kernel(double* __restrict__ A,
   __syncthreads();
   GPX_PANEL_STAMP(13);
   if (!panel) {
-    if (t == 0 && fail >= 0) atomicCAS(info, 0, k * NB + fail + 1);
-    const int nblk = gridDim.x + k;
-    double* Lkk = Dinv + (int64_t)(nblk + k) * NB * NB;  // scratch copy, moved into A by syrk_update
+    if (t == 0 && fail >= 0) atomicCAS(info, 0, c * NB + fail + 1);
+    double* Lcc = Dinv + (int64_t)(nblk + c) * NB * NB;  // scratch copy, moved into A by potrf_dinv
     for (int e = t; e < NB * NB; e += WG) {
-      const int r = e >> 6, c = e & 63;
-      Lkk[e] = (c <= r) ? sA[r * LD64 + c] : 0.0;
+      const int r = e >> 6, cc = e & 63;
+      Lcc[e] = (cc <= r) ? sA[r * LD64 + cc] : 0.0;
     }
     return;
   }
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const int e = (t + q * WG) * 2, r = e >> 6, c = e & 63;
-    *reinterpret_cast<double2*>(Aik + (int64_t)r * lda + c) = make_double2(sP[r * LD64 + c], sP[r * LD64 + c + 1]);
+    const int e = (t + q * WG) * 2, r = e >> 6, cc = e & 63;
+    *reinterpret_cast<double2*>(Aic + (int64_t)r * lda + cc) = make_double2(sP[r * LD64 + cc], sP[r * LD64 + cc + 1]);
   }
 }
 
-// Trailing update for block column k: tiles (i, j), k < j <= i < nblk, A_ij -= L_ik L_jk^T.
-// The last workgroup of the grid copies L_kk from the Dinv scratch into A_kk.
-__global__ void __launch_bounds__(WG) syrk_update_kernel(double* __restrict__ A, int64_t lda, int k, int nblk,
-                                                         const double* __restrict__ Dinv,
-                                                         const int32_t* __restrict__ info) {
-  if (*(volatile const int32_t*)info != 0) return;
-  if (blockIdx.x == gridDim.x - 1) {
-    const double* src = Dinv + (int64_t)(nblk + k) * NB * NB;
-    double* dst = A + (int64_t)k * NB * lda + (int64_t)k * NB;
-    for (int e = threadIdx.x; e < NB * NB / 2; e += WG) {
-      int r = e / (NB / 2), c2 = (e % (NB / 2)) * 2;
-      *reinterpret_cast<double2*>(dst + (int64_t)r * lda + c2) = *reinterpret_cast<const double2*>(src + r * NB + c2);
-    }
-    return;
+// Trailing workgroup: 128x128 tile `tile` of the lower triangle of block columns >= c+1, A_ij -= L_{i,c-1} L_{j,c-1}^T.
+// The 128-grid is aligned to the end of the matrix (first 64-block c0 = nblk - 2M); when it starts at block c, that
+// block row/column is computed but not stored (it belongs to this launch's panel).
+__device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t lda, int c, int nblk, int tile, double* lds) {
+  const int m = nblk - c - 1;
+  const int M = (m + 1) / 2;
+  const int c0 = nblk - 2 * M;
+  int I, J;
+  tri_decode(tile, I, J);
+  const int r0 = c0 + 2 * I, q0 = c0 + 2 * J;
+  const double* Li = A + (int64_t)r0 * NB * lda + (int64_t)(c - 1) * NB;
+  const double* Lj = A + (int64_t)q0 * NB * lda + (int64_t)(c - 1) * NB;
+  double* C = A + (int64_t)r0 * NB * lda + (int64_t)q0 * NB;
+  Tile128 tl;
+  tl.run(Li, lda, Lj, lda, 0, NB, lds);
+  // C - acc, stored for the 64-blocks (rb, cb) with cb >= c+1 and rb >= cb; loads of a row group first
+#pragma unroll
+  for (int i = 0; i < Tile128::WM; ++i) {
+    double cv[Tile128::WN][4];
+#pragma unroll
+    for (int j = 0; j < Tile128::WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cv[j][r] = C[(int64_t)Tile128::row_of(i, r) * lda + Tile128::col_of(j)];
+#pragma unroll
+    for (int j = 0; j < Tile128::WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = Tile128::row_of(i, r), col = Tile128::col_of(j);
+        const int rb = r0 + (row >> 6), cb = q0 + (col >> 6);
+        if (cb > c && rb >= cb) C[(int64_t)row * lda + col] = cv[j][r] - tl.acc[i][j][r];
+      }
   }
-  using Tile = MfmaTile<NB, NB, 16, false, false>;
-  __shared__ __attribute__((aligned(16))) double smem[Tile::LDS_DOUBLES];
-  int bi, bj;
-  tri_decode(blockIdx.x, bi, bj);
-  bi += k + 1;
-  bj += k + 1;
-  const double* Pi = A + (int64_t)bi * NB * lda + (int64_t)k * NB;  // L_ik (row-major, k contiguous)
-  const double* Pj = A + (int64_t)bj * NB * lda + (int64_t)k * NB;  // L_jk
-  double* C = A + (int64_t)bi * NB * lda + (int64_t)bj * NB;
-  // The C tile is read into registers up front, all loads in flight at once and overlapping the MFMA loop;
-  // a load-modify-store per element after the loop serialised 16 global round trips (41 us at step 0).
-  double cv[Tile::WM][Tile::WN][4];
-#pragma unroll
-  for (int i = 0; i < Tile::WM; ++i)
-#pragma unroll
-    for (int j = 0; j < Tile::WN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cv[i][j][r] = C[(int64_t)Tile::row_of(i, r) * lda + Tile::col_of(j)];
-  Tile tile;
-  tile.run(Pi, lda, Pj, lda, 0, NB, smem);
-#pragma unroll
-  for (int i = 0; i < Tile::WM; ++i)
-#pragma unroll
-    for (int j = 0; j < Tile::WN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        C[(int64_t)Tile::row_of(i, r) * lda + Tile::col_of(j)] = cv[i][j][r] - tile.acc[i][j][r];
 }
 
-// D_k = L_kk^{-1} for every diagonal block (one workgroup per block), into the first half of Dinv.
-__global__ void __launch_bounds__(WG) potrf_dinv_kernel(const double* __restrict__ A, int64_t lda,
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
+potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk,
+                                                        double* __restrict__ Dinv, int32_t* __restrict__ info,
+                                                        int first_wg) {
+  if (*(volatile int32_t*)info != 0) return;  // an earlier step failed: leave the rest untouched
+  __shared__ __attribute__((aligned(16))) double lds[STEP_LDS];
+  const int npanel = nblk - c;
+  const int b = first_wg + (int)blockIdx.x;
+  if (b < npanel)
+    panel_role(A, lda, c, b, nblk, Dinv, info, lds);
+  else
+    trailing_role(A, lda, c, nblk, b - npanel, lds);
+}
+
+// L_kk from the scratch into A, and D_k = L_kk^{-1} into the first half of Dinv (one workgroup per block).
+__global__ void __launch_bounds__(WG) potrf_dinv_kernel(double* __restrict__ A, int64_t lda, int nblk,
                                                         double* __restrict__ Dinv, const int32_t* __restrict__ info) {
   if (*(volatile const int32_t*)info != 0) return;
   __shared__ __attribute__((aligned(16))) double sL[NB * LD64];
   __shared__ __attribute__((aligned(16))) double sX[NB * LD64];
   __shared__ __attribute__((aligned(16))) double sT[NB * LD64];
   const int k = blockIdx.x, t = threadIdx.x;
-  const double* Lkk = A + (int64_t)k * NB * lda + (int64_t)k * NB;
+  const double* src = Dinv + (int64_t)(nblk + k) * NB * NB;
+  double* Lkk = A + (int64_t)k * NB * lda + (int64_t)k * NB;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int e = (t + q * WG) * 2, r = e >> 6, c = e & 63;
-    const double2 v = *reinterpret_cast<const double2*>(Lkk + (int64_t)r * lda + c);
+    const double2 v = *reinterpret_cast<const double2*>(src + r * NB + c);
+    *reinterpret_cast<double2*>(Lkk + (int64_t)r * lda + c) = v;
     sL[r * LD64 + c] = v.x;
     sL[r * LD64 + c + 1] = v.y;
   }
@@ -198,15 +250,18 @@ __global__ void __launch_bounds__(WG) potrf_dinv_kernel(const double* __restrict
   for (int e = t; e < NB * NB; e += WG) D[e] = sX[(e >> 6) * LD64 + (e & 63)];
 }
 
-hipError_t launch_potrf(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info) {
-  LaunchTimer tm(c, GPX_TIMER_POTRF);
+int potrf_step_grid(int c, int nblk) {
+  const int m = nblk - c - 1;
+  const int M = (c > 0 && m > 0) ? (m + 1) / 2 : 0;  // launch 0 has no trailing update
+  return (nblk - c) + M * (M + 1) / 2;
+}
+
+hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* Dinv, int32_t* info) {
+  LaunchTimer tm(ctx, GPX_TIMER_POTRF);
   const int nblk = npad / NB;
-  for (int k = 0; k < nblk; ++k) {
-    potrf_panel_kernel<<<nblk - k, WG, 0, c->stream>>>(A, lda, k, Dinv, info);
-    const int m = nblk - k - 1;
-    syrk_update_kernel<<<m * (m + 1) / 2 + 1, WG, 0, c->stream>>>(A, lda, k, nblk, Dinv, info);
-  }
-  potrf_dinv_kernel<<<nblk, WG, 0, c->stream>>>(A, lda, Dinv, info);
+  for (int c = 0; c < nblk; ++c)
+    potrf_step_kernel<<<potrf_step_grid(c, nblk), WG, 0, ctx->stream>>>(A, lda, c, nblk, Dinv, info, 0);
+  potrf_dinv_kernel<<<nblk, WG, 0, ctx->stream>>>(A, lda, nblk, Dinv, info);
   return hipGetLastError();
 }
 

@@ -13,7 +13,7 @@
 __device__ unsigned long long g_stamp[4][16];
 __device__ unsigned g_hwid[4];
 // wave-0 lane-0 timestamps of the panel phases, per wave w (lane 0): g_stamp[w][i]
-#define GPX_PANEL_STAMP(i) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 1) { g_stamp[threadIdx.x >> 6][i] = __builtin_readcyclecounter(); if (i == 0) g_hwid[threadIdx.x >> 6] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)); } } while (0)
+#define GPX_PANEL_STAMP(i) do { if ((threadIdx.x & 63) == 0 && blockIdx.x == 1 && c == 1) { g_stamp[threadIdx.x >> 6][i] = __builtin_readcyclecounter(); if (i == 0) g_hwid[threadIdx.x >> 6] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11)); } } while (0)
 namespace gpx {  // timers are no-ops in this harness
 LaunchTimer::LaunchTimer(Context* ctx, int t) : c(ctx), timer(t) {}
 LaunchTimer::~LaunchTimer() {}
@@ -34,7 +34,7 @@ __global__ void f16_test(const double* A, double* L, double* X, int* fail) {
 
   for (int e = threadIdx.x; e < 256; e += 64) sA[(e >> 4) * LD64 + (e & 15)] = A[e];
   __syncthreads();
-  const int f = chol16(sA, sD, 0);
+  const int f = chol16<LD64>(sA, sD, 0);
   __syncthreads();
   for (int e = threadIdx.x; e < 256; e += 64) { L[e] = sA[(e >> 4) * LD64 + (e & 15)]; X[e] = sD[(e >> 4) * LD64 + (e & 15)]; }
   if (threadIdx.x == 0) *fail = f;
@@ -127,17 +127,29 @@ int main(int argc, char** argv) {
     }
   }
   printf("n=%d full potrf: %.3f ms  info=%d  max|LL^T-A| (sampled rows)=%.3e  max|D L_kk - I|=%.3e\n", n, tp, hinfo, res, dres);
-  const float t1 = timeit([&] { for (int i = 0; i < 20; ++i) potrf_panel_kernel<<<1, WG>>>(A, n, 0, Dinv, info); }, 5);
-  const float t64 = timeit([&] { for (int i = 0; i < 20; ++i) potrf_panel_kernel<<<nblk, WG>>>(A, n, 0, Dinv, info); }, 5);
-  const float ts = timeit([&] { for (int i = 0; i < 20; ++i) syrk_update_kernel<<<(nblk - 1) * nblk / 2 + 1, WG>>>(A, n, 0, nblk, Dinv, info); }, 5);
-  const float ts60 = timeit([&] { for (int i = 0; i < 20; ++i) syrk_update_kernel<<<4 * 3 / 2 + 1, WG>>>(A, n, nblk - 4, nblk, Dinv, info); }, 5);
-  const float td = timeit([&] { for (int i = 0; i < 20; ++i) potrf_dinv_kernel<<<nblk, WG>>>(A, n, Dinv, info); }, 5);
-  printf("panel grid=1: %.2f us   panel grid=%d: %.2f us   syrk step0 (%d tiles): %.2f us   syrk step %d: %.2f us   dinv: %.2f us\n",
-         t1 * 50, nblk, t64 * 50, (nblk - 1) * nblk / 2, ts * 50, nblk - 4, ts60 * 50, td * 50);
+  // per-launch times of step c (after running steps 0..c-1 once): full grid, panel workgroups only
+  auto time_step = [&](int c, int mode) {  // 0 full grid, 1 panel workgroups only, 2 trailing workgroups only
+    CK(hipMemcpy(A, A0, (size_t)n * n * 8, hipMemcpyDeviceToDevice)); CK(hipMemset(info, 0, 4));
+    for (int cc = 0; cc < c; ++cc) potrf_step_kernel<<<potrf_step_grid(cc, nblk), WG>>>(A, n, cc, nblk, Dinv, info, 0);
+    CK(hipDeviceSynchronize());
+    const int full = potrf_step_grid(c, nblk);
+    const int grid = mode == 0 ? full : mode == 1 ? nblk - c : full - (nblk - c);
+    const int first = mode == 2 ? nblk - c : 0;
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < 20; ++i) potrf_step_kernel<<<grid, WG>>>(A, n, c, nblk, Dinv, info, first);
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    int hi; CK(hipMemcpy(&hi, info, 4, hipMemcpyDeviceToHost));
+    return hi ? -1.0f : ms * 50.0f;
+  };
+  const float td = timeit([&] { for (int i = 0; i < 20; ++i) potrf_dinv_kernel<<<nblk, WG>>>(A, n, nblk, Dinv, info); }, 5);
+  for (int c : {1, 8, 16, 32, 48, nblk - 3})
+    printf("step %2d: %6.2f us   panel wgs only %6.2f us   trailing wgs only %6.2f us (%d tiles)\n", c, time_step(c, 0),
+           time_step(c, 1), time_step(c, 2), potrf_step_grid(c, nblk) - (nblk - c));
+  printf("dinv: %.2f us\n", td * 50);
   CK(hipMemcpy(A, A0, (size_t)n * n * 8, hipMemcpyDeviceToDevice)); CK(hipMemset(info, 0, 4));
-  potrf_panel_kernel<<<nblk, WG>>>(A, n, 0, Dinv, info); CK(hipDeviceSynchronize());
-  CK(hipMemcpy(A, A0, (size_t)n * n * 8, hipMemcpyDeviceToDevice)); CK(hipMemset(info, 0, 4));
-  potrf_panel_kernel<<<nblk, WG>>>(A, n, 0, Dinv, info); CK(hipDeviceSynchronize());
+  potrf_step_kernel<<<potrf_step_grid(0, nblk), WG>>>(A, n, 0, nblk, Dinv, info, 0); CK(hipDeviceSynchronize());
+  potrf_step_kernel<<<potrf_step_grid(1, nblk), WG>>>(A, n, 1, nblk, Dinv, info, 0); CK(hipDeviceSynchronize());
   unsigned long long hs[4][16]; CK(hipMemcpyFromSymbol(hs, HIP_SYMBOL(g_stamp), sizeof(hs)));
   unsigned hw[4]; CK(hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_hwid), sizeof(hw)));
   for (int w = 0; w < 4; ++w) printf("wave %d HW_ID 0x%08x (simd %u, cu %u)\n", w, hw[w], (hw[w] >> 4) & 3, (hw[w] >> 8) & 15);
