@@ -96,6 +96,10 @@ _PROTOS = {
                               _p, _p, c_int64, _p, _p, _p, c_size_t]),
     "gpx_fit_f64_sync": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, c_int64, _p,
                                    c_int64, _p, _p, c_int64, _p, _p, _p, c_size_t, POINTER(c_int32)]),
+    "gpx_fit_batched_workspace_size": (c_int32, [c_int64, c_int64, c_int64, POINTER(c_size_t)]),
+    "gpx_fit_batched_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, c_int64, _p, c_int64, c_int64, _p,
+                                      c_int64, c_int64, c_int64, _p, c_int64, c_int64, _p, c_int64, _p, c_int64,
+                                      c_int64, _p, c_int64, _p, _p, c_size_t]),
     "gpx_sweep_workspace_size": (c_int32, [c_int64, c_int64, c_int64, POINTER(c_size_t)]),
     "gpx_posterior_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, _p, c_int64,
                                     _p, c_int64, c_int64, POINTER(c_double), POINTER(c_double), _p, c_int64, _p,

@@ -273,6 +273,74 @@ gpx_status gpx_fit_f64_sync(gpx_handle h, const gpx_kernel_params* p, int64_t n,
   return GPX_OK;
 }
 
+static size_t fit_slice_bytes(int64_t npad, int64_t nrhs) {
+  size_t a = trtri_ws(npad), b = alpha_ws(npad, nrhs);
+  return ((a > b ? a : b) + 255) & ~(size_t)255;
+}
+
+gpx_status gpx_fit_batched_workspace_size(int64_t n, int64_t nrhs, int64_t batch, size_t* bytes) {
+  if (!bytes || n < 1 || nrhs < 1 || nrhs > GPX_MAX_RHS || batch < 1 || batch > 65535) return GPX_INVALID_ARG;
+  *bytes = fit_slice_bytes(padded(n), nrhs) * (size_t)batch + 256;
+  return GPX_OK;
+}
+
+gpx_status gpx_fit_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n, const double* X,
+                               int64_t ldx, int64_t stride_x, const double* Y, int64_t ldy, int64_t stride_y,
+                               int64_t nrhs, double* K, int64_t ldk, int64_t stride_k, double* Dinv,
+                               int64_t stride_dinv, double* W, int64_t ldw, int64_t stride_w, double* alpha,
+                               int64_t stride_alpha, int32_t* info, void* ws, size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_TRY(check_params(c, p));
+  GPX_TRY(check_n(c, n));
+  if (batch < 1 || batch > 65535) return fail(c, GPX_INVALID_ARG, "batch must be in [1, 65535]");
+  if (nrhs < 1 || nrhs > GPX_MAX_RHS) return fail(c, GPX_INVALID_ARG, "nrhs must be in [1, 8]");
+  GPX_NONNULL(c, X);
+  GPX_NONNULL(c, Y);
+  GPX_NONNULL(c, K);
+  GPX_NONNULL(c, Dinv);
+  GPX_NONNULL(c, W);
+  GPX_NONNULL(c, alpha);
+  GPX_NONNULL(c, info);
+  GPX_NONNULL(c, ws);
+  const int64_t npad = padded(n);
+  GPX_TRY(check_ld(c, ldx, p->d, "X", false));
+  GPX_TRY(check_ld(c, ldy, nrhs, "Y", false));
+  GPX_TRY(check_ld(c, ldk, npad, "K", true));
+  GPX_TRY(check_ld(c, ldw, npad, "W", true));
+  const int64_t nblk = npad / gpx::NB;
+  if (batch > 1) {
+    // problems must not overlap (a stride of 0 would make them race on the same output)
+    if (stride_x < n * ldx || stride_y < n * ldy || stride_k < npad * ldk || stride_w < npad * ldw ||
+        stride_dinv < 2 * nblk * gpx::NB * gpx::NB || stride_alpha < npad * nrhs)
+      return fail(c, GPX_INVALID_ARG, "batch strides smaller than one problem");
+    if ((stride_k | stride_w | stride_dinv) & 1) return fail(c, GPX_INVALID_ARG, "K/W/Dinv strides must be even");
+  }
+  size_t need = 0;
+  GPX_TRY(gpx_fit_batched_workspace_size(n, nrhs, batch, &need));
+  if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "batched fit workspace too small");
+  GPX_TRY(use_device(c));
+  gpx::Batch bt;
+  bt.count = (int)batch;
+  bt.x = stride_x;
+  bt.y = stride_y;
+  bt.k = stride_k;
+  bt.dinv = stride_dinv;
+  bt.w = stride_w;
+  bt.alpha = stride_alpha;
+  bt.ws = (int64_t)(fit_slice_bytes(npad, nrhs) / sizeof(double));
+  double* slice = align256(ws);
+  GPX_TRY(hip_check(c, hipMemsetAsync(info, 0, sizeof(int32_t) * batch, c->stream), "memset info"));
+  GPX_TRY(hip_check(c, gpx::launch_gram(c, *p, (int)n, (int)npad, X, ldx, K, ldk, bt), "gram"));
+  GPX_TRY(hip_check(c, gpx::launch_potrf(c, (int)npad, K, ldk, Dinv, info, bt), "potrf"));
+  GPX_TRY(hip_check(c, gpx::launch_trtri(c, (int)npad, K, ldk, Dinv, W, ldw, slice, bt), "trtri"));
+  double* zpart = slice;
+  double* z = zpart + (size_t)(npad / 128) * npad * nrhs;
+  return hip_check(c, gpx::launch_alpha(c, (int)n, (int)npad, W, ldw, Y, ldy, (int)nrhs, p->const_mean, alpha, zpart, z,
+                                        bt),
+                   "alpha");
+}
+
 gpx_status gpx_mll_workspace_size(int64_t n, size_t* bytes) {
   if (!bytes || n < 1 || n > ((int64_t)1 << 20)) return GPX_INVALID_ARG;
   *bytes = gpx::mll_workspace_bytes(padded(n)) + 256;

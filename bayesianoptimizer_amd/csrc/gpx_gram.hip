@@ -12,7 +12,10 @@ namespace gpx {
 
 template <int DMAX, bool F32>
 __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, int nblk, const double* __restrict__ X,
-                                                  int64_t ldx, double* __restrict__ K, int64_t ldk) {
+                                                  int64_t ldx, double* __restrict__ K, int64_t ldk, int64_t sx,
+                                                  int64_t sk) {
+  X += blockIdx.y * sx;  // problem of a batched fit
+  K += blockIdx.y * sk;
   __shared__ double si[NB][DMAX + 1], sj[NB][DMAX + 1];    // scaled x / l
   __shared__ double ri[NB][DMAX + 1], rj[NB][DMAX + 1];    // raw x (linear kernel)
   int ti, tj;
@@ -83,13 +86,13 @@ __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, in
 }
 
 hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
-                       double* K, int64_t ldk) {
+                       double* K, int64_t ldk, const Batch& bt) {
   LaunchTimer tm(c, GPX_TIMER_GRAM);
   const int nblk = npad / NB;
-  const int tiles = nblk * (nblk + 1) / 2;
-#define GPX_GRAM(D)                                                                       \
-  (p.cov_fp32 ? gram_kernel<D, true><<<tiles, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk) \
-              : gram_kernel<D, false><<<tiles, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk))
+  const dim3 grid(nblk * (nblk + 1) / 2, bt.count);
+#define GPX_GRAM(D)                                                                                       \
+  (p.cov_fp32 ? gram_kernel<D, true><<<grid, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk, bt.x, bt.k) \
+              : gram_kernel<D, false><<<grid, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk, bt.x, bt.k))
   if (p.d <= 4)
     GPX_GRAM(4);
   else if (p.d <= 8)

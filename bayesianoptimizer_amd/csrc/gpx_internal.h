@@ -42,14 +42,25 @@ struct LaunchTimer {
   ~LaunchTimer();
 };
 
+// ---- batched fits -------------------------------------------------------------------------------
+// `count` independent problems of the same n / d / kernel parameters (restarts or seeds, BASELINE configs[3]) run in
+// the same launches: the problem index is one more grid dimension and every array of problem b starts at
+// base + b * stride (element strides; a workspace slice of `ws` doubles per problem).  count = 1: a single fit.
+struct Batch {
+  int count = 1;
+  int64_t x = 0, y = 0, k = 0, dinv = 0, w = 0, alpha = 0, ws = 0;
+};
+
 // ---- launch wrappers (defined in the .hip files) -------------------------------------------------
 hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
-                       double* K, int64_t ldk);
-hipError_t launch_potrf(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info);
+                       double* K, int64_t ldk, const Batch& bt = Batch());
+hipError_t launch_potrf(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info,
+                        const Batch& bt = Batch());
 hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, const double* Dinv, double* W,
-                        int64_t ldw, double* T);
+                        int64_t ldw, double* T, const Batch& bt = Batch());
 hipError_t launch_alpha(Context* c, int n, int npad, const double* W, int64_t ldw, const double* Y, int64_t ldy,
-                        int nrhs, double const_mean, double* alpha, double* zpart, double* z);
+                        int nrhs, double const_mean, double* alpha, double* zpart, double* z,
+                        const Batch& bt = Batch());
 
 struct SweepBuffers {
   double* kstar;     // npad x C

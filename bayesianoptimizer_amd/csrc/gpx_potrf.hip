@@ -213,9 +213,11 @@ __device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t ld
 }
 
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
-potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk,
-                                                        double* __restrict__ Dinv, int32_t* __restrict__ info,
-                                                        int first_wg) {
+potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, double* __restrict__ Dinv,
+                  int32_t* __restrict__ info, int first_wg, int64_t sa, int64_t sd) {
+  A += blockIdx.y * sa;  // problem of a batched fit
+  Dinv += blockIdx.y * sd;
+  info += blockIdx.y;
   if (*(volatile int32_t*)info != 0) return;  // an earlier step failed: leave the rest untouched
   __shared__ __attribute__((aligned(16))) double lds[STEP_LDS];
   const int npanel = nblk - c;
@@ -228,7 +230,11 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk,
 
 // L_kk from the scratch into A, and D_k = L_kk^{-1} into the first half of Dinv (one workgroup per block).
 __global__ void __launch_bounds__(WG) potrf_dinv_kernel(double* __restrict__ A, int64_t lda, int nblk,
-                                                        double* __restrict__ Dinv, const int32_t* __restrict__ info) {
+                                                        double* __restrict__ Dinv, const int32_t* __restrict__ info,
+                                                        int64_t sa, int64_t sd) {
+  A += blockIdx.y * sa;
+  Dinv += blockIdx.y * sd;
+  info += blockIdx.y;
   if (*(volatile const int32_t*)info != 0) return;
   __shared__ __attribute__((aligned(16))) double sL[NB * LD64];
   __shared__ __attribute__((aligned(16))) double sX[NB * LD64];
@@ -256,12 +262,13 @@ int potrf_step_grid(int c, int nblk) {
   return (nblk - c) + M * (M + 1) / 2;
 }
 
-hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* Dinv, int32_t* info) {
+hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt) {
   LaunchTimer tm(ctx, GPX_TIMER_POTRF);
   const int nblk = npad / NB;
   for (int c = 0; c < nblk; ++c)
-    potrf_step_kernel<<<potrf_step_grid(c, nblk), WG, 0, ctx->stream>>>(A, lda, c, nblk, Dinv, info, 0);
-  potrf_dinv_kernel<<<nblk, WG, 0, ctx->stream>>>(A, lda, nblk, Dinv, info);
+    potrf_step_kernel<<<dim3(potrf_step_grid(c, nblk), bt.count), WG, 0, ctx->stream>>>(A, lda, c, nblk, Dinv, info, 0,
+                                                                                         bt.k, bt.dinv);
+  potrf_dinv_kernel<<<dim3(nblk, bt.count), WG, 0, ctx->stream>>>(A, lda, nblk, Dinv, info, bt.k, bt.dinv);
   return hipGetLastError();
 }
 

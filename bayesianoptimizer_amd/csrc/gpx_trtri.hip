@@ -15,7 +15,9 @@
 namespace gpx {
 
 __global__ void __launch_bounds__(WG) trtri_diag_kernel(const double* __restrict__ Dinv, double* __restrict__ W,
-                                                        int64_t ldw) {
+                                                        int64_t ldw, int64_t sd, int64_t sw) {
+  Dinv += blockIdx.y * sd;  // problem of a batched fit
+  W += blockIdx.y * sw;
   const int b = blockIdx.x;
   const double* D = Dinv + (int64_t)b * NB * NB;
   double* Wbb = W + (int64_t)b * NB * ldw + (int64_t)b * NB;
@@ -29,13 +31,17 @@ __global__ void __launch_bounds__(WG) trtri_diag_kernel(const double* __restrict
   }
 }
 
-// T_p = L21^T W22 for group p of level with half-size h blocks.
+// T_p = L21^T W22 for group p of level with half-size h blocks.  blockIdx.z = group + groups * problem.
 __global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ L, int64_t ldl,
                                                      const double* __restrict__ W, int64_t ldw,
-                                                     double* __restrict__ T, int h, int nblk) {
+                                                     double* __restrict__ T, int h, int nblk, int groups, int64_t sl,
+                                                     int64_t sw, int64_t st) {
   using Tile = MfmaTile<NB, NB, 16, true, true>;
   __shared__ __attribute__((aligned(16))) double smem[Tile::LDS_DOUBLES];
-  const int p = blockIdx.z;
+  const int p = blockIdx.z % groups, prob = blockIdx.z / groups;
+  L += prob * sl;
+  W += prob * sw;
+  T += prob * st;
   const int s1 = p * 2 * h, s2 = s1 + h;
   const int nb2 = min(2 * h, nblk - s1) - h;
   const int rb = blockIdx.y, cb = blockIdx.x;
@@ -61,10 +67,12 @@ __global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ 
 
 // W12 = -W11 T_p
 __global__ void __launch_bounds__(WG) trtri_w_kernel(double* __restrict__ W, int64_t ldw, const double* __restrict__ T,
-                                                     int h, int nblk) {
+                                                     int h, int nblk, int groups, int64_t sw, int64_t st) {
   using Tile = MfmaTile<NB, NB, 16, false, true>;
   __shared__ __attribute__((aligned(16))) double smem[Tile::LDS_DOUBLES];
-  const int p = blockIdx.z;
+  const int p = blockIdx.z % groups, prob = blockIdx.z / groups;
+  W += prob * sw;
+  T += prob * st;
   const int s1 = p * 2 * h, s2 = s1 + h;
   const int nb2 = min(2 * h, nblk - s1) - h;
   const int rb = blockIdx.y, cb = blockIdx.x;
@@ -87,15 +95,15 @@ __global__ void __launch_bounds__(WG) trtri_w_kernel(double* __restrict__ W, int
 }
 
 hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, const double* Dinv, double* W,
-                        int64_t ldw, double* T) {
+                        int64_t ldw, double* T, const Batch& bt) {
   LaunchTimer tm(c, GPX_TIMER_TRTRI);
   const int nblk = npad / NB;
-  trtri_diag_kernel<<<nblk, WG, 0, c->stream>>>(Dinv, W, ldw);
+  trtri_diag_kernel<<<dim3(nblk, bt.count), WG, 0, c->stream>>>(Dinv, W, ldw, bt.dinv, bt.w);
   for (int h = 1; h < nblk; h *= 2) {
     const int groups = (nblk + 2 * h - 1) / (2 * h);
-    dim3 grid(h, h, groups);
-    trtri_t_kernel<<<grid, WG, 0, c->stream>>>(L, ldl, W, ldw, T, h, nblk);
-    trtri_w_kernel<<<grid, WG, 0, c->stream>>>(W, ldw, T, h, nblk);
+    dim3 grid(h, h, groups * bt.count);
+    trtri_t_kernel<<<grid, WG, 0, c->stream>>>(L, ldl, W, ldw, T, h, nblk, groups, bt.k, bt.w, bt.ws);
+    trtri_w_kernel<<<grid, WG, 0, c->stream>>>(W, ldw, T, h, nblk, groups, bt.w, bt.ws);
   }
   return hipGetLastError();
 }
@@ -106,7 +114,11 @@ constexpr int AK = 128;  // k-chunk of the z = W^T y pass
 // zpart[kc][i][r] = sum_{k in chunk kc, k <= i} W[k][i] * ytil[k][r]
 __global__ void __launch_bounds__(WG) alpha_z_kernel(int n, int npad, const double* __restrict__ W, int64_t ldw,
                                                      const double* __restrict__ Y, int64_t ldy, int nrhs,
-                                                     double const_mean, double* __restrict__ zpart) {
+                                                     double const_mean, double* __restrict__ zpart, int64_t sw,
+                                                     int64_t sy, int64_t sws) {
+  W += blockIdx.z * sw;  // problem of a batched fit
+  Y += blockIdx.z * sy;
+  zpart += blockIdx.z * sws;
   __shared__ double ys[AK][GPX_MAX_RHS];
   const int i = blockIdx.x * WG + threadIdx.x;
   const int kc = blockIdx.y;
@@ -135,7 +147,9 @@ __global__ void __launch_bounds__(WG) alpha_z_kernel(int n, int npad, const doub
 
 // z[i][r] = sum over valid chunks
 __global__ void __launch_bounds__(WG) alpha_zsum_kernel(int npad, int nrhs, const double* __restrict__ zpart,
-                                                        double* __restrict__ z) {
+                                                        double* __restrict__ z, int64_t sws) {
+  zpart += blockIdx.y * sws;
+  z += blockIdx.y * sws;
   const int e = blockIdx.x * WG + threadIdx.x;
   if (e >= npad * nrhs) return;
   const int i = e / nrhs;
@@ -146,8 +160,11 @@ __global__ void __launch_bounds__(WG) alpha_zsum_kernel(int npad, int nrhs, cons
 
 // alpha[k][r] = sum_{i >= k} W[k][i] z[i][r]; one wave per row k.
 __global__ void __launch_bounds__(WG) alpha_w_kernel(int n, int npad, const double* __restrict__ W, int64_t ldw,
-                                                     const double* __restrict__ z, int nrhs,
-                                                     double* __restrict__ alpha) {
+                                                     const double* __restrict__ z, int nrhs, double* __restrict__ alpha,
+                                                     int64_t sw, int64_t sws, int64_t sa) {
+  W += blockIdx.y * sw;
+  z += blockIdx.y * sws;
+  alpha += blockIdx.y * sa;
   const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (k >= npad) return;
@@ -171,12 +188,13 @@ __global__ void __launch_bounds__(WG) alpha_w_kernel(int n, int npad, const doub
 }
 
 hipError_t launch_alpha(Context* c, int n, int npad, const double* W, int64_t ldw, const double* Y, int64_t ldy,
-                        int nrhs, double const_mean, double* alpha, double* zpart, double* z) {
+                        int nrhs, double const_mean, double* alpha, double* zpart, double* z, const Batch& bt) {
   LaunchTimer tm(c, GPX_TIMER_ALPHA);
-  dim3 g1((npad + WG - 1) / WG, npad / AK);
-  alpha_z_kernel<<<g1, WG, 0, c->stream>>>(n, npad, W, ldw, Y, ldy, nrhs, const_mean, zpart);
-  alpha_zsum_kernel<<<(npad * nrhs + WG - 1) / WG, WG, 0, c->stream>>>(npad, nrhs, zpart, z);
-  alpha_w_kernel<<<(npad + 3) / 4, WG, 0, c->stream>>>(n, npad, W, ldw, z, nrhs, alpha);
+  dim3 g1((npad + WG - 1) / WG, npad / AK, bt.count);
+  alpha_z_kernel<<<g1, WG, 0, c->stream>>>(n, npad, W, ldw, Y, ldy, nrhs, const_mean, zpart, bt.w, bt.y, bt.ws);
+  alpha_zsum_kernel<<<dim3((npad * nrhs + WG - 1) / WG, bt.count), WG, 0, c->stream>>>(npad, nrhs, zpart, z, bt.ws);
+  alpha_w_kernel<<<dim3((npad + 3) / 4, bt.count), WG, 0, c->stream>>>(n, npad, W, ldw, z, nrhs, alpha, bt.w, bt.ws,
+                                                                        bt.alpha);
   return hipGetLastError();
 }
 

@@ -115,6 +115,7 @@ class GPState:
     n: int
     npad: int
     nrhs: int
+    _batch: Optional[tuple] = field(default=None, repr=False)  # stacked tensors of a fit_batched call
 
     @property
     def d(self) -> int:
@@ -233,6 +234,60 @@ class GPEngine:
             if piv >= 0:
                 raise NotPositiveDefiniteError(piv)
         return st
+
+    def fit_batched(self, X, Y, params: KernelParams, check: bool = True,
+                    out: Optional[Sequence[GPState]] = None) -> list:
+        """Posterior updates of B independent problems (X: B x n x d, Y: B x n or B x n x nrhs) sharing n, d and the
+        hyperparameters (restarts / seeds, BASELINE configs[3]) in the same launches (gpx_fit_batched_f64).  Returns
+        one GPState per problem (views into stacked device tensors); results equal B calls of ``fit``.  With
+        ``check`` synchronises and raises NotPositiveDefiniteError for the first failing problem."""
+        X = X if isinstance(X, torch.Tensor) else torch.as_tensor(X)
+        Y = Y if isinstance(Y, torch.Tensor) else torch.as_tensor(Y)
+        X = X.to(device=self.device, dtype=torch.float64).contiguous()
+        Y = Y.to(device=self.device, dtype=torch.float64)
+        if X.dim() != 3:
+            raise ValueError("X must be B x n x d")
+        if Y.dim() == 2:
+            Y = Y.unsqueeze(-1)
+        Y = Y.contiguous()
+        B, n, d = X.shape
+        if Y.shape[:2] != (B, n):
+            raise ValueError(f"Y must be {B} x {n} (x nrhs), got {tuple(Y.shape)}")
+        nrhs = Y.shape[2]
+        if not 1 <= nrhs <= _capi.GPX_MAX_RHS:
+            raise ValueError(f"number of outputs {nrhs} outside [1, {_capi.GPX_MAX_RHS}]")
+        pc = params.to_c(d)
+        npad = self.padded_n(n)
+        nblk = npad // 64
+        if out is not None and len(out) == B and all(s.n == n and s.nrhs == nrhs for s in out) and \
+                out[0]._batch is not None:
+            Lb, Wb, Db, Ab, Ib = out[0]._batch
+        else:
+            dev = self.device
+            Lb = torch.empty((B, npad, npad), dtype=torch.float64, device=dev)
+            Wb = torch.empty((B, npad, npad), dtype=torch.float64, device=dev)
+            Db = torch.empty((B, 2 * nblk, 64, 64), dtype=torch.float64, device=dev)
+            Ab = torch.empty((B, npad, nrhs), dtype=torch.float64, device=dev)
+            Ib = torch.zeros((B,), dtype=torch.int32, device=dev)
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_fit_batched_workspace_size(n, nrhs, B, ctypes.byref(nbytes)))
+        ws = self.workspace("fit_batched", nbytes.value)
+        self._bind_stream()
+        self._check(self.lib.gpx_fit_batched_f64(
+            self.handle, ctypes.byref(pc), B, n, _ptr(X), X.stride(1), X.stride(0), _ptr(Y), Y.stride(1), Y.stride(0),
+            nrhs, _ptr(Lb), npad, Lb.stride(0), _ptr(Db), Db.stride(0), _ptr(Wb), npad, Wb.stride(0), _ptr(Ab),
+            Ab.stride(0), _ptr(Ib), _ptr(ws), ws.numel()))
+        states = []
+        for b in range(B):
+            states.append(GPState(X=X[b], L=Lb[b], W=Wb[b], Dinv=Db[b], alpha=Ab[b], info=Ib[b:b + 1], params=params,
+                                  n=n, npad=npad, nrhs=nrhs, _batch=(Lb, Wb, Db, Ab, Ib)))
+        if check:
+            bad = Ib.cpu().numpy()
+            for b in range(B):
+                if bad[b]:
+                    raise NotPositiveDefiniteError(int(bad[b]) - 1, f"problem {b}: not positive definite at pivot "
+                                                                    f"{int(bad[b]) - 1}")
+        return states
 
     # individual stages (tests and benchmarks)
     def gram(self, X, params: KernelParams) -> torch.Tensor:

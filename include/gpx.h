@@ -154,6 +154,19 @@ gpx_status gpx_fit_f64_sync(gpx_handle h, const gpx_kernel_params* p, int64_t n,
                             double* W, int64_t ldw, double* alpha, int32_t* info, void* ws, size_t ws_bytes,
                             int32_t* info_host);
 
+/* Batched posterior updates: `batch` independent problems of the same n, d and kernel parameters (restarts /
+ * seeds: BASELINE configs[3], the per-batch `info` of the SURVEY §8b proposal) in the SAME launches, the problem
+ * index being one more grid dimension.  Every array of problem b starts at base + b * stride_* (element strides,
+ * >= one problem); info: device int32[batch], each 0 or that problem's failing pivot + 1.  Results are identical to
+ * `batch` calls of gpx_fit_f64.  The Cholesky is a latency-bound chain of nblk dependent launches, so a batch of B
+ * costs far less than B fits (replaces the per-restart fits of optimize_acqf / fit_gpytorch_mll restarts [upstream]). */
+gpx_status gpx_fit_batched_workspace_size(int64_t n, int64_t nrhs, int64_t batch, size_t* bytes);
+gpx_status gpx_fit_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n, const double* X,
+                               int64_t ldx, int64_t stride_x, const double* Y, int64_t ldy, int64_t stride_y,
+                               int64_t nrhs, double* K, int64_t ldk, int64_t stride_k, double* Dinv,
+                               int64_t stride_dinv, double* W, int64_t ldw, int64_t stride_w, double* alpha,
+                               int64_t stride_alpha, int32_t* info, void* ws, size_t ws_bytes);
+
 /* ---- posterior / acquisition ---------------------------------------------- */
 /* Posterior at m points Xs (m x d, ld ldxs): mean (m x nrhs, ld ldmean) and variance (m), untransformed
  * by (y_mean[r], y_scale[r]) per output r (host arrays of nrhs; NULL = identity).  Replaces

@@ -69,6 +69,11 @@ def test_workspace_queries_without_gpu(lib):
     assert lib.gpx_sweep_workspace_size(4096, 9, 10, ctypes.byref(b)) == _capi.GPX_INVALID_ARG
     assert lib.gpx_alpha_workspace_size(0, 1, ctypes.byref(b)) == _capi.GPX_INVALID_ARG
     assert lib.gpx_trtri_workspace_size(100, None) == _capi.GPX_INVALID_ARG
+    one = ctypes.c_size_t()
+    assert lib.gpx_fit_workspace_size(4096, 1, ctypes.byref(one)) == _capi.GPX_OK
+    assert lib.gpx_fit_batched_workspace_size(4096, 1, 4, ctypes.byref(b)) == _capi.GPX_OK
+    assert b.value >= 4 * one.value  # one workspace slice per problem
+    assert lib.gpx_fit_batched_workspace_size(4096, 1, 0, ctypes.byref(b)) == _capi.GPX_INVALID_ARG
 
 
 def test_null_handle_is_rejected(lib):

@@ -380,3 +380,43 @@ def test_config5_fp32_build_ucb_sweep(engine):
     # cond(K); the scores agree to ~1e-6 of their scale and the selected candidate is the same
     assert np.abs(sg - sref).max() <= 1e-5 * np.abs(sref).max()
     check_argmax(int(bi.item()), sref, sg, "config5 ucb")
+
+
+# ---- batched fits (BASELINE configs[3] shape) ------------------------------------------------------------
+@pytest.mark.parametrize("n,B,nrhs", [(300, 3, 1), (1000, 4, 2), (129, 5, 1)])
+def test_fit_batched_matches_single_fits_and_oracle(engine, n, B, nrhs):
+    d = 6
+    kp, op = pair("matern52", d, noise=2e-4)
+    Xs, Ys = [], []
+    for b in range(B):
+        X, y = O.synthetic_problem(n, d, 100 + b)
+        Xs.append(X)
+        Ys.append(np.stack([y * (r + 1) + r for r in range(nrhs)], axis=1))
+    sts = engine.fit_batched(t(np.stack(Xs)), t(np.stack(Ys)), kp)
+    for b in range(B):
+        single = engine.fit(t(Xs[b]), t(Ys[b]), kp)
+        # same kernels, same inputs: identical factor, inverse and alpha
+        assert torch.equal(torch.tril(sts[b].L[:n, :n]), torch.tril(single.L[:n, :n]))
+        assert torch.equal(torch.triu(sts[b].W), torch.triu(single.W))  # W is defined on its upper triangle
+        assert torch.equal(sts[b].alpha, single.alpha)
+        ost = O.fit(Xs[b], Ys[b], op)
+        a_r = ost.alpha.reshape(n, nrhs)
+        assert np.abs(sts[b].alpha[:n].cpu().numpy() - a_r).max() <= 1e-6 * np.abs(a_r).max()
+        Xq = O.sobol_candidates(64, d, b)
+        mu, var = engine.posterior(sts[b], t(Xq))
+        mu_r, var_r = O.posterior(ost, Xq)
+        check_posterior(mu.cpu().numpy(), var.cpu().numpy(), mu_r, var_r, O.kernel_diag(Xq, op))
+
+
+def test_fit_batched_reports_not_pd_per_problem(engine):
+    n, d, B = 200, 3, 3
+    Xs = np.stack([O.synthetic_problem(n, d, 7 + b)[0] for b in range(B)])
+    Xs[1, 1] = Xs[1, 0]  # exact duplicate in problem 1 only, no noise: 1 - 1*1 = 0 exactly at pivot 1
+    kp, op = pair("rbf", d, noise=1e-3)
+    kp = kp.replace(noise=0.0)
+    sts = engine.fit_batched(t(Xs), t(np.zeros((B, n))), kp.replace(noise=1e-3), check=False)
+    assert [st.pivot_failure() for st in sts] == [-1, -1, -1]
+    sts = engine.fit_batched(t(Xs), t(np.zeros((B, n))), kp, check=False)
+    assert [st.pivot_failure() for st in sts] == [-1, 1, -1]
+    with pytest.raises(NotPositiveDefiniteError):
+        engine.fit_batched(t(Xs), t(np.zeros((B, n))), kp)
