@@ -111,6 +111,16 @@ _PROTOS = {
     "gpx_mll_workspace_size": (c_int32, [c_int64, POINTER(c_size_t)]),
     "gpx_mll_grad_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, c_int64, _p,
                                    c_int64, _p, c_int64, _p, _p, _p, c_size_t]),
+    "gpx_svgp_prepare_workspace_size": (c_int32, [c_int64, c_int64, POINTER(c_size_t)]),
+    "gpx_svgp_prepare_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, c_int64, c_double, _p, c_int64, c_int64,
+                                       _p, c_int64, _p, c_int64, c_int64, _p, _p, _p, _p, _p, c_size_t]),
+    "gpx_svgp_predict_workspace_size": (c_int32, [c_int64, c_int64, POINTER(c_size_t)]),
+    "gpx_svgp_predict_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, c_int64, _p, c_int64, c_int64, _p, _p,
+                                       _p, _p, c_int64, c_int64, c_double, _p, c_int64, _p, c_int64, _p, _p,
+                                       c_size_t]),
+    "gpx_topk_workspace_size": (c_int32, [c_int64, POINTER(c_size_t)]),
+    "gpx_topk_f64": (c_int32, [_h, _p, c_int64, c_int64, _p, _p, _p, c_size_t]),
+    "gpx_fps_f64": (c_int32, [_h, _p, c_int64, c_int64, c_int64, c_int64, c_int64, _p]),
     "gpx_timing_enable": (c_int32, [_h, c_int32]),
     "gpx_timing_reset": (c_int32, [_h]),
     "gpx_timing_query": (c_int32, [_h, c_int32, POINTER(c_double), POINTER(c_int64)]),

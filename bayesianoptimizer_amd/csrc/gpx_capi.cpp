@@ -484,6 +484,191 @@ gpx_status gpx_argmax_combine_f64(gpx_handle h, const double* vals, const int64_
   return hip_check(c, gpx::launch_argmax_final(c, vals, idx, count, best_val, best_idx), "argmax_combine");
 }
 
+// ---- SVGP predictive + pool-scan selection --------------------------------------
+namespace {
+struct SvgpPrepLayout {
+  size_t L, dinv, slice, spad, mpad, total;  // byte offsets / sizes per task (256-aligned)
+};
+size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+SvgpPrepLayout svgp_prep_layout(int64_t Mpad) {
+  SvgpPrepLayout l;
+  const size_t L = al256((size_t)Mpad * Mpad * 8);
+  const size_t D = al256((size_t)2 * (Mpad / gpx::NB) * gpx::NB * gpx::NB * 8);
+  const size_t fs = al256(trtri_ws(Mpad) > alpha_ws(Mpad, 1) ? trtri_ws(Mpad) : alpha_ws(Mpad, 1));
+  l.L = 0;
+  l.dinv = L;
+  l.slice = L + D;
+  l.spad = L + D + fs;
+  l.mpad = l.spad + L;
+  l.total = l.mpad + al256((size_t)Mpad * 8);
+  return l;
+}
+gpx_status check_svgp(Context* c, const gpx_kernel_params* p, int64_t ntask, int64_t M) {
+  if (ntask < 1 || ntask > 64) return fail(c, GPX_INVALID_ARG, "ntask must be in [1, 64]");
+  if (M < 1 || M > 65536) return fail(c, GPX_INVALID_ARG, "number of inducing points must be in [1, 65536]");
+  if (!p) return fail(c, GPX_INVALID_ARG, "kernel params pointer is NULL");
+  for (int64_t t = 0; t < ntask; ++t) {
+    GPX_TRY(check_params(c, p + t));
+    if (p[t].d != p[0].d) return fail(c, GPX_INVALID_ARG, "all tasks must share the input dimension");
+  }
+  return GPX_OK;
+}
+}  // namespace
+
+gpx_status gpx_svgp_prepare_workspace_size(int64_t M, int64_t ntask, size_t* bytes) {
+  if (!bytes || M < 1 || ntask < 1) return GPX_INVALID_ARG;
+  *bytes = svgp_prep_layout(padded(M)).total * (size_t)ntask + 256;
+  return GPX_OK;
+}
+
+gpx_status gpx_svgp_prepare_f64(gpx_handle h, const gpx_kernel_params* p, int64_t ntask, int64_t M, double jitter,
+                                const double* Z, int64_t ldz, int64_t stride_z, const double* vmean,
+                                int64_t stride_m, const double* vchol, int64_t ldc, int64_t stride_c, double* W,
+                                double* W2, double* alpha, int32_t* info, void* ws, size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_TRY(check_svgp(c, p, ntask, M));
+  GPX_NONNULL(c, Z);
+  GPX_NONNULL(c, vmean);
+  GPX_NONNULL(c, vchol);
+  GPX_NONNULL(c, W);
+  GPX_NONNULL(c, W2);
+  GPX_NONNULL(c, alpha);
+  GPX_NONNULL(c, info);
+  GPX_NONNULL(c, ws);
+  if (!(jitter >= 0.0)) return fail(c, GPX_INVALID_ARG, "jitter must be non-negative");
+  GPX_TRY(check_ld(c, ldz, p[0].d, "Z", false));
+  GPX_TRY(check_ld(c, ldc, M, "chol_variational_covar", false));
+  if (ntask > 1 && (stride_z < M * ldz || stride_m < M || stride_c < M * ldc))
+    return fail(c, GPX_INVALID_ARG, "task strides smaller than one task");
+  const int64_t Mpad = padded(M);
+  size_t need = 0;
+  GPX_TRY(gpx_svgp_prepare_workspace_size(M, ntask, &need));
+  if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "svgp prepare workspace too small");
+  GPX_TRY(use_device(c));
+  const SvgpPrepLayout lay = svgp_prep_layout(Mpad);
+  char* base = reinterpret_cast<char*>(align256(ws));
+  auto at = [&](int64_t t, size_t off) { return reinterpret_cast<double*>(base + lay.total * t + off); };
+  const int64_t tstride = (int64_t)(lay.total / sizeof(double));  // elements between tasks in the workspace
+  GPX_TRY(hip_check(c, hipMemsetAsync(info, 0, sizeof(int32_t) * ntask, c->stream), "memset info"));
+  // K_ZZ + jitter I per task (the hyperparameters differ per task; the likelihood noise is not part of K_ZZ)
+  for (int64_t t = 0; t < ntask; ++t) {
+    gpx_kernel_params q = p[t];
+    q.noise = 0.0;
+    q.jitter = jitter;
+    GPX_TRY(hip_check(c, gpx::launch_gram(c, q, (int)M, (int)Mpad, Z + t * stride_z, ldz, at(t, lay.L), Mpad), "gram"));
+  }
+  gpx::Batch bt;
+  bt.count = (int)ntask;
+  bt.k = tstride;
+  bt.dinv = tstride;
+  bt.ws = tstride;
+  bt.w = Mpad * Mpad;
+  GPX_TRY(hip_check(c, gpx::launch_potrf(c, (int)Mpad, at(0, lay.L), Mpad, at(0, lay.dinv), info, bt), "potrf"));
+  GPX_TRY(hip_check(c, gpx::launch_trtri(c, (int)Mpad, at(0, lay.L), Mpad, at(0, lay.dinv), W, Mpad, at(0, lay.slice),
+                                         bt),
+                    "trtri"));
+  // zero-padded m and S = tril(chol) in the workspace, then alpha' = W m and W2 = W S
+  GPX_TRY(hip_check(c, gpx::launch_svgp_pad(c, (int)ntask, (int)M, (int)Mpad, vmean, stride_m, vchol, ldc, stride_c,
+                                            at(0, lay.mpad), at(0, lay.spad), tstride),
+                    "svgp pad"));
+  gpx::Batch tv;
+  tv.count = (int)ntask;
+  tv.w = Mpad * Mpad;
+  tv.y = tstride;
+  tv.alpha = Mpad;
+  GPX_TRY(hip_check(c, gpx::launch_trmv_upper(c, (int)Mpad, W, Mpad, at(0, lay.mpad), alpha, tv), "alpha'"));
+  return hip_check(c, gpx::launch_svgp_w2(c, (int)ntask, (int)Mpad, W, at(0, lay.spad), tstride, W2), "svgp W2");
+}
+
+gpx_status gpx_svgp_predict_workspace_size(int64_t M, int64_t m, size_t* bytes) {
+  if (!bytes || M < 1 || m < 1) return GPX_INVALID_ARG;
+  const int64_t Mpad = padded(M);
+  const int64_t C = gpx::sweep_chunk_size(Mpad, m);
+  *bytes = gpx::sweep_workspace_bytes(Mpad, 1, m) + (size_t)(Mpad / 128) * C * 8 + 512;
+  return GPX_OK;
+}
+
+gpx_status gpx_svgp_predict_f64(gpx_handle h, const gpx_kernel_params* p, int64_t ntask, int64_t M, const double* Z,
+                                int64_t ldz, int64_t stride_z, const double* W, const double* W2, const double* alpha,
+                                const double* Xs, int64_t m, int64_t ldxs, double min_var, double* mean_out,
+                                int64_t ldmean, double* var_out, int64_t ldvar, double* score_out, void* ws,
+                                size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_TRY(check_svgp(c, p, ntask, M));
+  GPX_NONNULL(c, Z);
+  GPX_NONNULL(c, W);
+  GPX_NONNULL(c, W2);
+  GPX_NONNULL(c, alpha);
+  GPX_NONNULL(c, Xs);
+  GPX_NONNULL(c, ws);
+  if (m < 1) return fail(c, GPX_INVALID_ARG, "m must be >= 1");
+  if (!mean_out && !var_out && !score_out) return fail(c, GPX_INVALID_ARG, "no output requested");
+  if (!(min_var >= 0.0)) return fail(c, GPX_INVALID_ARG, "min_var must be non-negative");
+  GPX_TRY(check_ld(c, ldz, p[0].d, "Z", false));
+  GPX_TRY(check_ld(c, ldxs, p[0].d, "Xs", false));
+  if (mean_out) GPX_TRY(check_ld(c, ldmean, ntask, "mean", false));
+  if (var_out) GPX_TRY(check_ld(c, ldvar, ntask, "var", false));
+  if (ntask > 1 && stride_z < M * ldz) return fail(c, GPX_INVALID_ARG, "task stride of Z smaller than one task");
+  const int64_t Mpad = padded(M);
+  size_t need = 0;
+  GPX_TRY(gpx_svgp_predict_workspace_size(M, m, &need));
+  if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "svgp predict workspace too small");
+  gpx::SweepBuffers b;
+  GPX_TRY(carve_sweep(c, Mpad, 1, m, ws, ws_bytes, &b));
+  double* ss2 = reinterpret_cast<double*>(((uintptr_t)(b.rec_idx + (m + 255) / 256 + 1) + 255) & ~(uintptr_t)255);
+  GPX_TRY(use_device(c));
+  for (int64_t s = 0; s < m; s += b.chunk) {
+    const int64_t mc = (m - s) < b.chunk ? (m - s) : b.chunk;
+    for (int64_t t = 0; t < ntask; ++t) {
+      GPX_TRY(hip_check(c,
+                        gpx::launch_svgp_chunk(c, p[t], min_var, (int)t, (int)M, (int)Mpad, Z + t * stride_z, ldz,
+                                               W + t * Mpad * Mpad, W2 + t * Mpad * Mpad, Mpad, alpha + t * Mpad,
+                                               Xs + s * ldxs, ldxs, mc, b, ss2, mean_out ? mean_out + s * ldmean : nullptr,
+                                               ldmean, var_out ? var_out + s * ldvar : nullptr, ldvar,
+                                               score_out ? score_out + s : nullptr),
+                        "svgp predict"));
+    }
+  }
+  return GPX_OK;
+}
+
+gpx_status gpx_topk_workspace_size(int64_t m, size_t* bytes) {
+  if (!bytes || m < 1 || m > ((int64_t)1 << 30)) return GPX_INVALID_ARG;
+  *bytes = gpx::topk_workspace_bytes(m);
+  return GPX_OK;
+}
+
+gpx_status gpx_topk_f64(gpx_handle h, const double* scores, int64_t m, int64_t k, int64_t* idx_out, double* val_out,
+                        void* ws, size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_NONNULL(c, scores);
+  GPX_NONNULL(c, idx_out);
+  GPX_NONNULL(c, ws);
+  if (m < 1 || m > ((int64_t)1 << 30)) return fail(c, GPX_INVALID_ARG, "m must be in [1, 2^30]");
+  if (k < 1 || k > m) return fail(c, GPX_INVALID_ARG, "k must be in [1, m]");
+  if (ws_bytes < gpx::topk_workspace_bytes(m)) return fail(c, GPX_INVALID_ARG, "topk workspace too small");
+  GPX_TRY(use_device(c));
+  return hip_check(c, gpx::launch_topk(c, scores, m, k, idx_out, val_out, ws, ws_bytes), "topk");
+}
+
+gpx_status gpx_fps_f64(gpx_handle h, const double* X, int64_t m, int64_t d, int64_t ldx, int64_t k, int64_t start,
+                       int64_t* idx_out) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_NONNULL(c, X);
+  GPX_NONNULL(c, idx_out);
+  if (m < 1 || m > 32 * 1024) return fail(c, GPX_INVALID_ARG, "fps supports 1 <= m <= 32768 points");
+  if (d < 1 || d > GPX_MAX_DIM) return fail(c, GPX_INVALID_ARG, "d must be in [1, 32]");
+  if (k < 1 || k > m) return fail(c, GPX_INVALID_ARG, "k must be in [1, m]");
+  if (start < 0 || start >= m) return fail(c, GPX_INVALID_ARG, "start index outside [0, m)");
+  GPX_TRY(check_ld(c, ldx, d, "X", false));
+  GPX_TRY(use_device(c));
+  return hip_check(c, gpx::launch_fps(c, X, m, (int)d, ldx, k, start, idx_out), "fps");
+}
+
 gpx_status gpx_timing_enable(gpx_handle h, int32_t mask) {
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return GPX_INVALID_ARG;

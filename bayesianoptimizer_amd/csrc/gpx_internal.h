@@ -80,6 +80,26 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
 hipError_t launch_argmax_final(Context* c, const double* vals, const int64_t* idx, int64_t count, double* best_val,
                                int64_t* best_idx);
 
+// SVGP predictive of one task over a chunk (gpx_sweep.hip); ss2: (Mpad/128) x C partials of the full W2 product.
+hipError_t launch_svgp_chunk(Context* c, const gpx_kernel_params& p, double min_var, int task, int M, int Mpad,
+                             const double* Z, int64_t ldz, const double* W, const double* W2, int64_t ldw,
+                             const double* alpha, const double* Xs, int64_t ldxs, int64_t m_chunk,
+                             const SweepBuffers& b, double* ss2, double* mean_out, int64_t ldmean, double* var_out,
+                             int64_t ldvar, double* score);
+// SVGP preparation helpers (gpx_svgp.hip)
+hipError_t launch_svgp_pad(Context* c, int ntask, int M, int Mpad, const double* vmean, int64_t stride_m,
+                           const double* vchol, int64_t ldc, int64_t stride_c, double* mpad, double* spad,
+                           int64_t sdst);
+hipError_t launch_trmv_upper(Context* c, int npad, const double* W, int64_t ldw, const double* z, double* out,
+                             const Batch& bt);
+hipError_t launch_svgp_w2(Context* c, int ntask, int Mpad, const double* W, const double* S, int64_t s_stride,
+                          double* W2);
+size_t topk_workspace_bytes(int64_t m);
+hipError_t launch_topk(Context* c, const double* scores, int64_t m, int64_t k, int64_t* idx_out, double* val_out,
+                       void* ws, size_t ws_bytes);
+hipError_t launch_fps(Context* c, const double* X, int64_t m, int d, int64_t ldx, int64_t k, int64_t start,
+                      int64_t* idx_out);
+
 size_t mll_workspace_bytes(int64_t npad);
 hipError_t launch_mll(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
                       const double* Y, int64_t ldy, int nrhs, const double* L, int64_t ldl, const double* W,

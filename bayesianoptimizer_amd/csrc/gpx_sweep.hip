@@ -160,9 +160,11 @@ __global__ void __launch_bounds__(WG) kstar_kernel(gpx_kernel_params p, int n, c
 constexpr int TT = 128;  // trmm tile (rows of V x candidates)
 using TrmmTile = MfmaTile<TT, TT, 16, true, true>;
 
+// kfull = 0: W upper triangular (k < (I+1)*128); kfull = 1: W is a full npad x npad matrix (the SVGP's
+// W2 = L^{-T} S term, gpx_svgp.hip), k over all nI row tiles.
 __global__ void __launch_bounds__(WG) trmm_sumsq_kernel(const double* __restrict__ W, int64_t ldw,
                                                         const double* __restrict__ kstar, int64_t C, int nI, int ncb,
-                                                        double* __restrict__ ss_part) {
+                                                        double* __restrict__ ss_part, int kfull) {
   __shared__ __attribute__((aligned(16))) double smem[TrmmTile::LDS_DOUBLES];
   // Heaviest row tiles first.  XCD-aware when the candidate tiles split evenly over the 8 XCDs: workgroups
   // b, b+8, ... share an XCD (dispatch is round-robin; speed only, never correctness), so XCD x gets the
@@ -181,7 +183,7 @@ __global__ void __launch_bounds__(WG) trmm_sumsq_kernel(const double* __restrict
   const double* Ab = W + (int64_t)I * TT;            // A(m=i,k) = W[k][I*128 + i]
   const double* Bb = kstar + (int64_t)cb * TT;       // B(k,n=c) = K*[k][cb*128 + c]
   TrmmTile tile;
-  tile.run(Ab, ldw, Bb, C, 0, (I + 1) * TT, smem);
+  tile.run(Ab, ldw, Bb, C, 0, (kfull ? nI : I + 1) * TT, smem);
   // column sums of squares over this wave's rows, then over the lanes holding the same column
   double s[TrmmTile::WN];
 #pragma unroll
@@ -379,7 +381,7 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
   {
     LaunchTimer tm(c, GPX_TIMER_TRMM);
     const int ncbt = (int)((m_chunk + TT - 1) / TT);
-    trmm_sumsq_kernel<<<ncbt * nI, WG, 0, c->stream>>>(W, ldw, b.kstar, C, nI, ncbt, b.ss_part);
+    trmm_sumsq_kernel<<<ncbt * nI, WG, 0, c->stream>>>(W, ldw, b.kstar, C, nI, ncbt, b.ss_part, 0);
   }
   {
     LaunchTimer tm(c, GPX_TIMER_ACQ);
@@ -400,6 +402,76 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
                                                    b.ss_part, mean_out, ldmean, var_out, scores_out,
                                                    b.rec_val + rec_offset, b.rec_idx + rec_offset,
                                                    index_offset);
+  }
+  return hipGetLastError();
+}
+
+// ---- SVGP predictive: one task of Bayesian7's batched SVGP over a chunk --------------------
+// mean = const + K_*Z alpha' (alpha' = L^{-T} m), var = k** - |L^{-1} k*|^2 + |S^T L^{-1} k*|^2 + noise, i.e. the
+// whitened VariationalStrategy predictive k** + k*^T L^{-T} (S S^T - I) L^{-1} k* plus the GaussianLikelihood noise
+// [upstream]; score (optional) accumulates sum_t var_t over the tasks (the pool-scan score, Bayesian7.py:671).
+__global__ void __launch_bounds__(WG) svgp_finalize_kernel(gpx_kernel_params p, double min_var, int task,
+                                                           const double* __restrict__ Xs, int64_t ldxs,
+                                                           int64_t m_chunk, int64_t C, int nJB, int nI,
+                                                           const double* __restrict__ mu_part,
+                                                           const double* __restrict__ ss1,
+                                                           const double* __restrict__ ss2,
+                                                           double* __restrict__ mean_out, int64_t ldmean,
+                                                           double* __restrict__ var_out, int64_t ldvar,
+                                                           double* __restrict__ score) {
+  const int64_t c = (int64_t)blockIdx.x * WG + threadIdx.x;
+  if (c >= m_chunk) return;
+  double kd = p.outputscale;
+  if (p.kind == GPX_KERNEL_SCALE_LINEAR_MATERN52) {
+    double lv = 0.0;
+    for (int k = 0; k < p.d; ++k) {
+      const double v = Xs[c * ldxs + k];
+      lv += v * v * p.linear_variance[k];
+    }
+    kd = p.outputscale * (lv + 1.0);
+  }
+  const double s1 = sum_partials(ss1 + c, nI, C);
+  const double s2 = sum_partials(ss2 + c, nI, C);
+  const double var = fmax(kd - s1 + s2 + p.noise, min_var);
+  const double mu = sum_partials(mu_part + c, nJB, C) + p.const_mean;
+  if (mean_out) mean_out[c * ldmean + task] = mu;
+  if (var_out) var_out[c * ldvar + task] = var;
+  if (score) score[c] = (task == 0 ? 0.0 : score[c]) + var;
+}
+
+hipError_t launch_svgp_chunk(Context* c, const gpx_kernel_params& p, double min_var, int task, int M, int Mpad,
+                             const double* Z, int64_t ldz, const double* W, const double* W2, int64_t ldw,
+                             const double* alpha, const double* Xs, int64_t ldxs, int64_t m_chunk,
+                             const SweepBuffers& b, double* ss2, double* mean_out, int64_t ldmean, double* var_out,
+                             int64_t ldvar, double* score) {
+  const int64_t C = b.chunk;
+  const int nJB = Mpad / NB, nI = Mpad / TT;
+  const int ncb = (int)((m_chunk + WG - 1) / WG);
+  {
+    LaunchTimer tm(c, GPX_TIMER_KSTAR);
+    dim3 g(ncb, nJB);
+#define GPX_KSTAR(D) kstar_kernel<D, false><<<g, WG, 0, c->stream>>>(p, M, Z, ldz, alpha, 1, Xs, ldxs, m_chunk, C, \
+                                                                      b.kstar, b.mu_part)
+    if (p.d <= 4)
+      GPX_KSTAR(4);
+    else if (p.d <= 8)
+      GPX_KSTAR(8);
+    else if (p.d <= 16)
+      GPX_KSTAR(16);
+    else
+      GPX_KSTAR(32);
+#undef GPX_KSTAR
+  }
+  {
+    LaunchTimer tm(c, GPX_TIMER_TRMM);
+    const int ncbt = (int)((m_chunk + TT - 1) / TT);
+    trmm_sumsq_kernel<<<ncbt * nI, WG, 0, c->stream>>>(W, ldw, b.kstar, C, nI, ncbt, b.ss_part, 0);
+    trmm_sumsq_kernel<<<ncbt * nI, WG, 0, c->stream>>>(W2, ldw, b.kstar, C, nI, ncbt, ss2, 1);
+  }
+  {
+    LaunchTimer tm(c, GPX_TIMER_ACQ);
+    svgp_finalize_kernel<<<ncb, WG, 0, c->stream>>>(p, min_var, task, Xs, ldxs, m_chunk, C, nJB, nI, b.mu_part,
+                                                    b.ss_part, ss2, mean_out, ldmean, var_out, ldvar, score);
   }
   return hipGetLastError();
 }

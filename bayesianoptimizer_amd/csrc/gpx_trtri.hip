@@ -198,4 +198,13 @@ hipError_t launch_alpha(Context* c, int n, int npad, const double* W, int64_t ld
   return hipGetLastError();
 }
 
+// out = W z for an upper-triangular W and one right-hand side of npad entries (the SVGP's alpha' = L^{-T} m),
+// batched over problems with strides bt.w (W), bt.y (z), bt.alpha (out).
+hipError_t launch_trmv_upper(Context* c, int npad, const double* W, int64_t ldw, const double* z, double* out,
+                             const Batch& bt) {
+  alpha_w_kernel<<<dim3((npad + 3) / 4, bt.count), WG, 0, c->stream>>>(npad, npad, W, ldw, z, 1, out, bt.w, bt.y,
+                                                                        bt.alpha);
+  return hipGetLastError();
+}
+
 }  // namespace gpx

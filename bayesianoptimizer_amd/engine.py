@@ -438,6 +438,86 @@ class GPEngine:
         }
         return res, state
 
+    # -- SVGP predictive + pool-scan selection --------------------------------
+    def svgp_prepare(self, params: Sequence[KernelParams], Z, vmean, vchol, jitter: float = 1e-4):
+        """Factor K_ZZ + jitter I per task and build the predictive caches of a trained batched SVGP
+        (gpx_svgp_prepare_f64).  Z: T x M x d, vmean: T x M, vchol: T x M x M (lower triangle used).  Returns a dict
+        of device tensors (W, W2, alpha, info, Z) consumed by ``svgp_predict``; raises NotPositiveDefiniteError."""
+        Z = torch.as_tensor(Z).to(device=self.device, dtype=torch.float64).contiguous()
+        vmean = torch.as_tensor(vmean).to(device=self.device, dtype=torch.float64).contiguous()
+        vchol = torch.as_tensor(vchol).to(device=self.device, dtype=torch.float64).contiguous()
+        T, M, d = Z.shape
+        if vmean.shape != (T, M) or vchol.shape != (T, M, M):
+            raise ValueError("vmean must be T x M and vchol T x M x M")
+        if len(params) != T:
+            raise ValueError(f"expected {T} kernel parameter sets, got {len(params)}")
+        pcs = (KernelParamsC * T)(*[pp.to_c(d) for pp in params])
+        Mpad = self.padded_n(M)
+        W = torch.empty((T, Mpad, Mpad), dtype=torch.float64, device=self.device)
+        W2 = torch.empty((T, Mpad, Mpad), dtype=torch.float64, device=self.device)
+        alpha = torch.empty((T, Mpad), dtype=torch.float64, device=self.device)
+        info = torch.zeros((T,), dtype=torch.int32, device=self.device)
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_svgp_prepare_workspace_size(M, T, ctypes.byref(nbytes)))
+        ws = self.workspace("svgp_prep", nbytes.value)
+        self._bind_stream()
+        self._check(self.lib.gpx_svgp_prepare_f64(
+            self.handle, pcs, T, M, float(jitter), _ptr(Z), Z.stride(1), Z.stride(0), _ptr(vmean), vmean.stride(0),
+            _ptr(vchol), vchol.stride(1), vchol.stride(0), _ptr(W), _ptr(W2), _ptr(alpha), _ptr(info), _ptr(ws),
+            ws.numel()))
+        bad = info.cpu().numpy()
+        for t in range(T):
+            if bad[t]:
+                raise NotPositiveDefiniteError(int(bad[t]) - 1, f"task {t}: K_ZZ not positive definite at pivot "
+                                                                f"{int(bad[t]) - 1}")
+        return {"Z": Z, "W": W, "W2": W2, "alpha": alpha, "params": list(params), "M": M}
+
+    def svgp_predict(self, prep: dict, Xs, min_var: float = 1e-10, want=("mean", "var", "score")):
+        """Predictive mean / variance (m x T, likelihood noise included) and the pool-scan score (m, sum over tasks
+        of the variance) at input-transformed points Xs (gpx_svgp_predict_f64)."""
+        Xs = self._as_f64(Xs, "Xs")
+        Z = prep["Z"]
+        T, M, d = Z.shape
+        if Xs.shape[1] != d:
+            raise ValueError(f"Xs has {Xs.shape[1]} columns, model has d={d}")
+        m = Xs.shape[0]
+        mean = torch.empty((m, T), dtype=torch.float64, device=self.device) if "mean" in want else None
+        var = torch.empty((m, T), dtype=torch.float64, device=self.device) if "var" in want else None
+        score = torch.empty((m,), dtype=torch.float64, device=self.device) if "score" in want else None
+        pcs = (KernelParamsC * T)(*[pp.to_c(d) for pp in prep["params"]])
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_svgp_predict_workspace_size(M, m, ctypes.byref(nbytes)))
+        ws = self.workspace("svgp_pred", nbytes.value)
+        self._bind_stream()
+        self._check(self.lib.gpx_svgp_predict_f64(
+            self.handle, pcs, T, M, _ptr(Z), Z.stride(1), Z.stride(0), _ptr(prep["W"]), _ptr(prep["W2"]),
+            _ptr(prep["alpha"]), _ptr(Xs), m, Xs.stride(0), float(min_var), _ptr(mean), T, _ptr(var), T, _ptr(score),
+            _ptr(ws), ws.numel()))
+        return mean, var, score
+
+    def topk(self, scores: torch.Tensor, k: int):
+        """(values, indices) of the k largest scores, descending, ties -> lower index first (gpx_topk_f64)."""
+        scores = scores.to(device=self.device, dtype=torch.float64).contiguous().reshape(-1)
+        m = scores.numel()
+        idx = torch.empty((k,), dtype=torch.int64, device=self.device)
+        val = torch.empty((k,), dtype=torch.float64, device=self.device)
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_topk_workspace_size(m, ctypes.byref(nbytes)))
+        ws = self.workspace("topk", nbytes.value)
+        self._bind_stream()
+        self._check(self.lib.gpx_topk_f64(self.handle, _ptr(scores), m, int(k), _ptr(idx), _ptr(val), _ptr(ws),
+                                          ws.numel()))
+        return val, idx
+
+    def fps(self, X, k: int, start: int) -> torch.Tensor:
+        """Indices (selection order) of k farthest-point-sampled rows of X starting at row ``start`` (gpx_fps_f64)."""
+        X = self._as_f64(X, "X")
+        m, d = X.shape
+        idx = torch.empty((k,), dtype=torch.int64, device=self.device)
+        self._bind_stream()
+        self._check(self.lib.gpx_fps_f64(self.handle, _ptr(X), m, d, X.stride(0), int(k), int(start), _ptr(idx)))
+        return idx
+
     # -- instrumentation ------------------------------------------------------------------------
     def timing_enable(self, timers: Sequence[str] = ("trmm",)):
         mask = 0

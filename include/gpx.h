@@ -213,6 +213,43 @@ gpx_status gpx_mll_grad_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n,
                             const double* W, int64_t ldw, const double* alpha, double* out, void* ws,
                             size_t ws_bytes);
 
+/* ---- SVGP predictive + pool-scan selection: the driven variant ---------------- */
+/* optimization/Bayesian7.py's BatchSVGP (ntask outputs, each with its own ScaleKernel(Linear + Matérn-5/2)
+ * hyperparameters p[t], ConstantMean p[t].const_mean and GaussianLikelihood noise p[t].noise) served from its trained
+ * variational state: inducing points Z (ntask x M x d), variational mean m (ntask x M) and chol_variational_covar
+ * (ntask x M x M, only its lower triangle is used, like CholeskyVariationalDistribution [upstream]).
+ *
+ * gpx_svgp_prepare_f64 (once per trained model) factors K_ZZ + jitter I per task (gpytorch's VariationalStrategy
+ * jitter: 1e-4 for the reference's float32 model [upstream]) and stores per task, in padded Mpad x Mpad blocks
+ * (Mpad = gpx_padded_n(M)): W = L_ZZ^{-T}, W2 = W S, and alpha' = W m (Mpad entries).  info: int32[ntask].
+ * gpx_svgp_predict_f64 evaluates the whitened predictive of every task at m points Xs (already input-transformed,
+ * Bayesian7.py:181-190): mean = const + k*^T alpha', var = max(k** - |W^T k*|^2 + |W2^T k*|^2 + noise, min_var)
+ * (= likelihood(model(x)).variance, Bayesian7.py:558,668) into mean_out / var_out (m x ntask, NULL = skip) and
+ * score_out[m] = sum over tasks of var (the pool-scan uncertainty score, Bayesian7.py:671; NULL = skip). */
+gpx_status gpx_svgp_prepare_workspace_size(int64_t M, int64_t ntask, size_t* bytes);
+gpx_status gpx_svgp_prepare_f64(gpx_handle h, const gpx_kernel_params* p, int64_t ntask, int64_t M, double jitter,
+                                const double* Z, int64_t ldz, int64_t stride_z, const double* vmean,
+                                int64_t stride_m, const double* vchol, int64_t ldc, int64_t stride_c, double* W,
+                                double* W2, double* alpha, int32_t* info, void* ws, size_t ws_bytes);
+gpx_status gpx_svgp_predict_workspace_size(int64_t M, int64_t m, size_t* bytes);
+gpx_status gpx_svgp_predict_f64(gpx_handle h, const gpx_kernel_params* p, int64_t ntask, int64_t M, const double* Z,
+                                int64_t ldz, int64_t stride_z, const double* W, const double* W2, const double* alpha,
+                                const double* Xs, int64_t m, int64_t ldxs, double min_var, double* mean_out,
+                                int64_t ldmean, double* var_out, int64_t ldvar, double* score_out, void* ws,
+                                size_t ws_bytes);
+
+/* The k largest scores in descending order (replaces torch.topk, Bayesian7.py:681): stable, so equal scores keep
+ * the lower index first; NaN ranks last.  idx_out: int64[k], val_out: double[k] (NULL = skip). */
+gpx_status gpx_topk_workspace_size(int64_t m, size_t* bytes);
+gpx_status gpx_topk_f64(gpx_handle h, const double* scores, int64_t m, int64_t k, int64_t* idx_out, double* val_out,
+                        void* ws, size_t ws_bytes);
+
+/* Greedy farthest point sampling of k of the m points X (m <= 32768), starting at index `start` (the reference
+ * draws it with torch.randint): farthest_point_sampling of Bayesian7.py:82-106.  Squared Euclidean distances in
+ * fp64, argmax with the lowest index among ties (torch.argmax).  idx_out: int64[k], the selection order. */
+gpx_status gpx_fps_f64(gpx_handle h, const double* X, int64_t m, int64_t d, int64_t ldx, int64_t k, int64_t start,
+                       int64_t* idx_out);
+
 /* ---- instrumentation ------------------------------------------------------------------------------ */
 /* For every timer whose bit is set in `mask`, each launch of that kernel family is bracketed by hipEvents
  * on the handle's stream; totals are read with gpx_timing_query (synchronises the stream). mask 0 = off. */

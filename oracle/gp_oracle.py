@@ -24,6 +24,10 @@ What it restates (fp64, NumPy/SciPy):
 * a8  Argmax with the lowest index winning ties (``optimization/Bayesian.py:117``,
       ``optimization/Bayesian7.py:681,724-727``).
 * §8f row 1: -log p(y) and its gradient w.r.t. the kernel hyperparameters (``mll_value_grad``).
+* a9 / §8f row 2: the batched SVGP predictive of ``optimization/Bayesian7.py:543-563,664-671`` (gpytorch's whitened
+      ``VariationalStrategy`` [upstream]: mean = c + k*^T L^{-T} m, var = k** + k*^T L^{-T}(S S^T - I)L^{-1} k* +
+      noise), the torch.topk of ``:681`` (stable, descending) and ``farthest_point_sampling`` of ``:82-106``
+      (``svgp_predict``, ``topk_desc``, ``farthest_point_sampling``).
 * a1/a2 input/output transforms of ``optimization/Bayesian7.py:181-190,363-385``.
 
 Parity status: **parity unpinned**.  The reference delegates this arithmetic to GPyTorch /
@@ -417,3 +421,65 @@ def sobol_candidates(m: int, d: int, seed: int):
     eng = qmc.Sobol(d, scramble=True, seed=seed)
     k = int(math.ceil(math.log2(max(m, 1))))
     return eng.random_base2(k)[:m]
+
+
+# ---------------------------------------------------------------------------------------------
+# a9 / §8f row 2: batched SVGP predictive + pool-scan selection (optimization/Bayesian7.py)
+# ---------------------------------------------------------------------------------------------
+VARIATIONAL_JITTER_F32 = 1e-4  # gpytorch settings.variational_cholesky_jitter, float32 [upstream]
+
+
+def svgp_predict(Z, vmean, vchol, params: Sequence[KernelParams], Xs, jitter=VARIATIONAL_JITTER_F32,
+                 min_var=GPYTORCH_MIN_VAR_F64):
+    """Per task t (``optimization/Bayesian7.py:137-178`` BatchSVGP, whitened VariationalStrategy [upstream]):
+    L = chol(K_ZZ + jitter I), A = L^{-1} K_ZX, mean = c_t + A^T m_t,
+    var = k(x, x) + colsum(A * ((S S^T - I) A)) + noise_t  (S = tril(chol_variational_covar)),
+    floored at ``min_var`` (gpytorch MultivariateNormal.variance [upstream]).  Returns mean, var (m x T) and the
+    pool-scan score sum_t var (``optimization/Bayesian7.py:671``)."""
+    T = len(params)
+    Xs = np.asarray(Xs, dtype=np.float64)
+    mean = np.empty((Xs.shape[0], T))
+    var = np.empty((Xs.shape[0], T))
+    for t in range(T):
+        p = params[t]
+        Zt = np.asarray(Z[t], dtype=np.float64)
+        Kzz = kernel_matrix(Zt, Zt, p)
+        Kzz[np.diag_indices_from(Kzz)] += jitter
+        L = cholesky(Kzz)
+        A = sla.solve_triangular(L, kernel_matrix(Zt, Xs, p), lower=True, check_finite=False)
+        S = np.tril(np.asarray(vchol[t], dtype=np.float64))
+        SA = S.T @ A
+        mean[:, t] = p.const_mean + A.T @ np.asarray(vmean[t], dtype=np.float64)
+        v = kernel_diag(Xs, p) - np.einsum("ij,ij->j", A, A) + np.einsum("ij,ij->j", SA, SA) + p.noise
+        var[:, t] = np.maximum(v, min_var)
+    return mean, var, var.sum(axis=1)
+
+
+def topk_desc(scores, k):
+    """The k largest scores, descending; equal scores keep the lower index first; NaN ranks last (torch.topk of
+    ``optimization/Bayesian7.py:681`` with a deterministic tie order)."""
+    s = np.asarray(scores, dtype=np.float64)
+    key = np.where(np.isnan(s), -np.inf, s)
+    order = np.argsort(-key, kind="stable")[:k]
+    return key[order], order
+
+
+def farthest_point_sampling(X, k, start):
+    """Greedy FPS (``optimization/Bayesian7.py:82-106``) from index ``start``: squared Euclidean distances (fp64,
+    summed over dimensions in order), argmax with the lowest index among ties (torch.argmax).  Returns the selected
+    indices in selection order."""
+    X = np.asarray(X, dtype=np.float64)
+
+    def sqdist(c):
+        d2 = np.zeros(X.shape[0])
+        for j in range(X.shape[1]):  # dimension order, like the device loop
+            d2 += (X[:, j] - X[c, j]) ** 2
+        return d2
+
+    idx = [int(start)]
+    dist = sqdist(start)
+    for _ in range(1, k):
+        far = int(np.argmax(dist))
+        idx.append(far)
+        dist = np.minimum(dist, sqdist(far))
+    return np.asarray(idx, dtype=np.int64)
