@@ -100,6 +100,9 @@ _PROTOS = {
     "gpx_fit_batched_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, c_int64, _p, c_int64, c_int64, _p,
                                       c_int64, c_int64, c_int64, _p, c_int64, c_int64, _p, c_int64, _p, c_int64,
                                       c_int64, _p, c_int64, _p, _p, c_size_t]),
+    "gpx_append_workspace_size": (c_int32, [c_int64, c_int64, c_int64, POINTER(c_size_t)]),
+    "gpx_append_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, c_int64, _p, c_int64, _p, c_int64, c_int64, _p,
+                                 c_int64, _p, _p, c_int64, _p, _p, _p, c_size_t]),
     "gpx_sweep_workspace_size": (c_int32, [c_int64, c_int64, c_int64, POINTER(c_size_t)]),
     "gpx_posterior_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, _p, c_int64,
                                     _p, c_int64, c_int64, POINTER(c_double), POINTER(c_double), _p, c_int64, _p,

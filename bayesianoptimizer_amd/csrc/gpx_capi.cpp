@@ -273,6 +273,51 @@ gpx_status gpx_fit_f64_sync(gpx_handle h, const gpx_kernel_params* p, int64_t n,
   return GPX_OK;
 }
 
+gpx_status gpx_append_workspace_size(int64_t n_old, int64_t n_new, int64_t nrhs, size_t* bytes) {
+  if (!bytes || n_old < 1 || n_new <= n_old || nrhs < 1 || nrhs > GPX_MAX_RHS) return GPX_INVALID_ARG;
+  size_t a = gpx::append_workspace_bytes(n_old, n_new), b = alpha_ws(padded(n_new), nrhs);
+  *bytes = (a > b ? a : b) + 256;
+  return GPX_OK;
+}
+
+gpx_status gpx_append_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n_old, int64_t n_new, const double* X,
+                          int64_t ldx, const double* Y, int64_t ldy, int64_t nrhs, double* L, int64_t ldl,
+                          double* Dinv, double* W, int64_t ldw, double* alpha, int32_t* info, void* ws,
+                          size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_TRY(check_params(c, p));
+  GPX_TRY(check_n(c, n_new));
+  if (n_old < 1 || n_new <= n_old) return fail(c, GPX_INVALID_ARG, "append needs 1 <= n_old < n_new");
+  if (nrhs < 1 || nrhs > GPX_MAX_RHS) return fail(c, GPX_INVALID_ARG, "nrhs must be in [1, 8]");
+  GPX_NONNULL(c, X);
+  GPX_NONNULL(c, Y);
+  GPX_NONNULL(c, L);
+  GPX_NONNULL(c, Dinv);
+  GPX_NONNULL(c, W);
+  GPX_NONNULL(c, alpha);
+  GPX_NONNULL(c, info);
+  GPX_NONNULL(c, ws);
+  const int64_t npad = padded(n_new);
+  GPX_TRY(check_ld(c, ldx, p->d, "X", false));
+  GPX_TRY(check_ld(c, ldy, nrhs, "Y", false));
+  GPX_TRY(check_ld(c, ldl, npad, "L", true));
+  GPX_TRY(check_ld(c, ldw, npad, "W", true));
+  size_t need = 0;
+  GPX_TRY(gpx_append_workspace_size(n_old, n_new, nrhs, &need));
+  if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "append workspace too small");
+  GPX_TRY(use_device(c));
+  double* base = align256(ws);
+  GPX_TRY(hip_check(c, hipMemsetAsync(info, 0, sizeof(int32_t), c->stream), "memset info"));
+  GPX_TRY(hip_check(c, gpx::launch_append(c, *p, (int)n_old, (int)n_new, X, ldx, L, ldl, Dinv, W, ldw, info, base),
+                    "append"));
+  double* zpart = base;
+  double* z = zpart + (size_t)(npad / 128) * npad * nrhs;
+  return hip_check(c, gpx::launch_alpha(c, (int)n_new, (int)npad, W, ldw, Y, ldy, (int)nrhs, p->const_mean, alpha,
+                                        zpart, z),
+                   "alpha");
+}
+
 static size_t fit_slice_bytes(int64_t npad, int64_t nrhs) {
   size_t a = trtri_ws(npad), b = alpha_ws(npad, nrhs);
   return ((a > b ? a : b) + 255) & ~(size_t)255;

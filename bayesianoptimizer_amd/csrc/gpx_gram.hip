@@ -2,6 +2,7 @@
 // SURVEY §8a row a3 — replaces the covar_module(X) evaluation inside GPyTorch's ExactGP path [upstream]
 // (optimization/Bayesian.py:91-93, optimization/Bayesian6.py:471-484).
 //
+// With rb0 > 0 only the tiles of row blocks >= rb0 are built (the new rows of an incremental update).
 // HBM-write-bound: each 64x64 tile is written once (32 KiB); inputs are two 64 x d slices of X staged in
 // LDS (lengthscale-divided copy for the stationary part, raw copy for the linear part).  Each wave owns
 // one row of the tile at a time and writes 64 consecutive doubles (512 B) per store instruction.
@@ -11,7 +12,7 @@
 namespace gpx {
 
 template <int DMAX, bool F32>
-__global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, int nblk, const double* __restrict__ X,
+__global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, int t0, const double* __restrict__ X,
                                                   int64_t ldx, double* __restrict__ K, int64_t ldk, int64_t sx,
                                                   int64_t sk) {
   X += blockIdx.y * sx;  // problem of a batched fit
@@ -19,7 +20,7 @@ __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, in
   __shared__ double si[NB][DMAX + 1], sj[NB][DMAX + 1];    // scaled x / l
   __shared__ double ri[NB][DMAX + 1], rj[NB][DMAX + 1];    // raw x (linear kernel)
   int ti, tj;
-  tri_decode(blockIdx.x, ti, tj);
+  tri_decode(t0 + (int)blockIdx.x, ti, tj);
   const int i0 = ti * NB, j0 = tj * NB;
   const int d = p.d;
   const bool lin = (p.kind == GPX_KERNEL_SCALE_LINEAR_MATERN52);
@@ -86,13 +87,14 @@ __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, in
 }
 
 hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
-                       double* K, int64_t ldk, const Batch& bt) {
+                       double* K, int64_t ldk, const Batch& bt, int rb0) {
   LaunchTimer tm(c, GPX_TIMER_GRAM);
   const int nblk = npad / NB;
-  const dim3 grid(nblk * (nblk + 1) / 2, bt.count);
+  const int t0 = rb0 * (rb0 + 1) / 2;  // tiles of the row blocks above rb0 are skipped (gpx_append_f64)
+  const dim3 grid(nblk * (nblk + 1) / 2 - t0, bt.count);
 #define GPX_GRAM(D)                                                                                       \
-  (p.cov_fp32 ? gram_kernel<D, true><<<grid, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk, bt.x, bt.k) \
-              : gram_kernel<D, false><<<grid, WG, 0, c->stream>>>(p, n, nblk, X, ldx, K, ldk, bt.x, bt.k))
+  (p.cov_fp32 ? gram_kernel<D, true><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k) \
+              : gram_kernel<D, false><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k))
   if (p.d <= 4)
     GPX_GRAM(4);
   else if (p.d <= 8)

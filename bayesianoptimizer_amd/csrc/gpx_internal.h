@@ -53,7 +53,7 @@ struct Batch {
 
 // ---- launch wrappers (defined in the .hip files) -------------------------------------------------
 hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
-                       double* K, int64_t ldk, const Batch& bt = Batch());
+                       double* K, int64_t ldk, const Batch& bt = Batch(), int rb0 = 0);
 hipError_t launch_potrf(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info,
                         const Batch& bt = Batch());
 hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, const double* Dinv, double* W,
@@ -99,6 +99,10 @@ hipError_t launch_topk(Context* c, const double* scores, int64_t m, int64_t k, i
                        void* ws, size_t ws_bytes);
 hipError_t launch_fps(Context* c, const double* X, int64_t m, int d, int64_t ldx, int64_t k, int64_t start,
                       int64_t* idx_out);
+
+hipError_t launch_append(Context* c, const gpx_kernel_params& p, int n_old, int n_new, const double* X, int64_t ldx,
+                         double* L, int64_t ldl, double* Dinv, double* W, int64_t ldw, int32_t* info, double* ws);
+size_t append_workspace_bytes(int64_t n_old, int64_t n_new);
 
 size_t mll_workspace_bytes(int64_t npad);
 hipError_t launch_mll(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,

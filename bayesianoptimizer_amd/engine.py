@@ -102,7 +102,9 @@ class GPState:
     """Device-resident posterior caches of one exact GP (all tensors on the engine's device).
 
     L: padded lower Cholesky factor (only its lower triangle is defined), W = L^{-T} (upper), alpha =
-    K^{-1}(Y - m) (padded_n x nrhs), Dinv: inverses of the 64x64 diagonal blocks of L.
+    K^{-1}(Y - m) (padded_n x nrhs), Dinv: inverses of the 64x64 diagonal blocks of L.  L and W may be
+    npad x npad views of larger capacity x capacity buffers (``GPEngine.append`` grows into them); their
+    leading dimension is ``L.stride(0)``.
     """
 
     X: torch.Tensor
@@ -190,25 +192,30 @@ class GPEngine:
         return ((n + _capi.GPX_TILE - 1) // _capi.GPX_TILE) * _capi.GPX_TILE
 
     # -- fit --------------------------------------------------------------------------------------
-    def alloc_state(self, X: torch.Tensor, nrhs: int, params: KernelParams) -> GPState:
+    def alloc_state(self, X: torch.Tensor, nrhs: int, params: KernelParams, capacity: int = 0) -> GPState:
+        """Device buffers of one GP; ``capacity`` (training points) reserves room for later ``append`` calls."""
         n = X.shape[0]
         npad = self.padded_n(n)
-        nblk = npad // 64
+        cap = max(npad, self.padded_n(capacity)) if capacity else npad
         dev = self.device
+        Lbuf = torch.empty((cap, cap), dtype=torch.float64, device=dev)
+        Wbuf = torch.empty((cap, cap), dtype=torch.float64, device=dev)
         return GPState(
             X=X,
-            L=torch.empty((npad, npad), dtype=torch.float64, device=dev),
-            W=torch.empty((npad, npad), dtype=torch.float64, device=dev),
-            Dinv=torch.empty((2 * nblk, 64, 64), dtype=torch.float64, device=dev),
+            L=Lbuf[:npad, :npad],
+            W=Wbuf[:npad, :npad],
+            Dinv=torch.empty((2 * (cap // 64), 64, 64), dtype=torch.float64, device=dev),
             alpha=torch.empty((npad, nrhs), dtype=torch.float64, device=dev),
             info=torch.zeros((1,), dtype=torch.int32, device=dev),
             params=params, n=n, npad=npad, nrhs=nrhs)
 
-    def fit(self, X, Y, params: KernelParams, check: bool = True, out: Optional[GPState] = None) -> GPState:
+    def fit(self, X, Y, params: KernelParams, check: bool = True, out: Optional[GPState] = None,
+            capacity: int = 0) -> GPState:
         """One posterior update: Gram + blocked Cholesky + L^{-T} + alpha for up to 8 outputs sharing X.
 
         With ``check`` (default) synchronises and raises NotPositiveDefiniteError like psd_safe_cholesky
-        would; with ``check=False`` stays asynchronous (inspect ``state.info`` later).
+        would; with ``check=False`` stays asynchronous (inspect ``state.info`` later).  ``capacity``: training
+        points to reserve buffer room for (later ``append`` calls grow in place up to it).
         """
         X = self._as_f64(X, "X")
         Y = self._as_f64(Y, "Y")
@@ -219,7 +226,8 @@ class GPEngine:
         if not 1 <= nrhs <= _capi.GPX_MAX_RHS:
             raise ValueError(f"number of outputs {nrhs} outside [1, {_capi.GPX_MAX_RHS}]")
         pc = params.to_c(d)
-        st = out if (out is not None and out.n == n and out.nrhs == nrhs) else self.alloc_state(X, nrhs, params)
+        st = out if (out is not None and out.n == n and out.nrhs == nrhs) else \
+            self.alloc_state(X, nrhs, params, capacity)
         st.X, st.params = X, params
         nbytes = ctypes.c_size_t()
         self._check(self.lib.gpx_fit_workspace_size(n, nrhs, ctypes.byref(nbytes)))
@@ -227,13 +235,62 @@ class GPEngine:
         self._bind_stream()
         self._check(self.lib.gpx_fit_f64(
             self.handle, ctypes.byref(pc), n, _ptr(X), X.stride(0), _ptr(Y), Y.stride(0), nrhs,
-            _ptr(st.L), st.npad, _ptr(st.Dinv), _ptr(st.W), st.npad, _ptr(st.alpha), _ptr(st.info),
+            _ptr(st.L), st.L.stride(0), _ptr(st.Dinv), _ptr(st.W), st.W.stride(0), _ptr(st.alpha), _ptr(st.info),
             _ptr(ws), ws.numel()))
         if check:
             piv = st.pivot_failure()
             if piv >= 0:
                 raise NotPositiveDefiniteError(piv)
         return st
+
+    def append(self, state: GPState, X, Y, check: bool = True, growth: float = 1.5) -> GPState:
+        """Incremental posterior update: X / Y hold ALL training rows, the first ``state.n`` of them
+        the ones ``state`` was fitted on (same hyperparameters).  The bordered Cholesky of the new rows
+        (gpx_append_f64, O(n^2 q)) replaces the reference's refit from scratch after appending observations
+        (optimization/Bayesian7.py:628-631,639; optimization/Bayesian.py:163-174).  Y may be re-standardised: alpha is
+        recomputed from all of it.  Grows the buffers (by ``growth``) when the capacity is exceeded.  Returns the
+        updated state (the same object when it fitted in place)."""
+        X = self._as_f64(X, "X")
+        Y = self._as_f64(Y, "Y")
+        n_new, d = X.shape
+        n_old = state.n
+        if d != state.d:
+            raise ValueError(f"X has {d} columns, state has d={state.d}")
+        if Y.shape != (n_new, state.nrhs):
+            raise ValueError(f"Y must have shape ({n_new}, {state.nrhs}), got {tuple(Y.shape)}")
+        if n_new <= n_old:
+            raise ValueError(f"append needs more rows than the fitted {n_old}, got {n_new}")
+        npad = self.padded_n(n_new)
+        ld = state.L.stride(0)
+        if npad > ld or state.Dinv.shape[0] < 2 * (npad // 64) or state.W.stride(0) != ld:
+            # grow: copy the kept leading block into bigger buffers (plumbing; the update itself is gpx_append_f64)
+            cap = self.padded_n(max(n_new, int(growth * n_new)))
+            n0 = (n_old // _capi.GPX_TILE) * _capi.GPX_TILE
+            new = self.alloc_state(X, state.nrhs, state.params, cap)
+            Lb = new.L.as_strided((cap, cap), (cap, 1))
+            Wb = new.W.as_strided((cap, cap), (cap, 1))
+            Lb[:n0, :n0].copy_(state.L[:n0, :n0])
+            Wb[:n0, :n0].copy_(state.W[:n0, :n0])
+            new.Dinv[: n0 // 64].copy_(state.Dinv[: n0 // 64])
+            state, ld = new, cap
+        Lfull = state.L.as_strided((npad, npad), (ld, 1))
+        Wfull = state.W.as_strided((npad, npad), (ld, 1))
+        alpha = torch.empty((npad, state.nrhs), dtype=torch.float64, device=self.device)
+        pc = state.params.to_c(d)
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_append_workspace_size(n_old, n_new, state.nrhs, ctypes.byref(nbytes)))
+        ws = self.workspace("append", nbytes.value)
+        self._bind_stream()
+        self._check(self.lib.gpx_append_f64(
+            self.handle, ctypes.byref(pc), n_old, n_new, _ptr(X), X.stride(0), _ptr(Y), Y.stride(0), state.nrhs,
+            _ptr(Lfull), ld, _ptr(state.Dinv), _ptr(Wfull), ld, _ptr(alpha), _ptr(state.info), _ptr(ws), ws.numel()))
+        state.X, state.L, state.W, state.alpha = X, Lfull, Wfull, alpha
+        state.n, state.npad, state._batch = n_new, npad, None
+        if check:
+            piv = state.pivot_failure()
+            if piv >= 0:
+                raise NotPositiveDefiniteError(piv)
+        return state
 
     def fit_batched(self, X, Y, params: KernelParams, check: bool = True,
                     out: Optional[Sequence[GPState]] = None) -> list:
@@ -340,7 +397,7 @@ class GPEngine:
         pc = state.params.to_c(state.d)
         self._bind_stream()
         self._check(self.lib.gpx_posterior_f64(
-            self.handle, ctypes.byref(pc), state.n, _ptr(state.X), state.X.stride(0), _ptr(state.W), state.npad,
+            self.handle, ctypes.byref(pc), state.n, _ptr(state.X), state.X.stride(0), _ptr(state.W), state.W.stride(0),
             _ptr(state.alpha), state.nrhs, _ptr(Xs), m, Xs.stride(0), ym, ys, _ptr(mean), state.nrhs, _ptr(var),
             _ptr(ws), ws.numel()))
         return mean, var
@@ -373,7 +430,7 @@ class GPEngine:
         pc = state.params.to_c(state.d)
         self._bind_stream()
         self._check(self.lib.gpx_acquire_argmax_f64(
-            self.handle, ctypes.byref(pc), state.n, _ptr(state.X), state.X.stride(0), _ptr(state.W), state.npad,
+            self.handle, ctypes.byref(pc), state.n, _ptr(state.X), state.X.stride(0), _ptr(state.W), state.W.stride(0),
             _ptr(alpha), _ptr(Xs), m, Xs.stride(0), ctypes.byref(ap), int(index_offset), _ptr(best_val),
             _ptr(best_idx), _ptr(scores), _ptr(ws), ws.numel()))
         if return_scores:
@@ -407,7 +464,7 @@ class GPEngine:
         self._bind_stream()
         self._check(self.lib.gpx_mll_grad_f64(
             self.handle, ctypes.byref(pc), state.n, _ptr(state.X), state.X.stride(0), _ptr(Y), Y.stride(0),
-            state.nrhs, _ptr(state.L), state.npad, _ptr(state.W), state.npad, _ptr(state.alpha), _ptr(out),
+            state.nrhs, _ptr(state.L), state.L.stride(0), _ptr(state.W), state.W.stride(0), _ptr(state.alpha), _ptr(out),
             _ptr(ws), ws.numel()))
         return out
 

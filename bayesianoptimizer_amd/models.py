@@ -96,6 +96,32 @@ class ExactGP:
         self.mll_result = res
         return self.fit()
 
+    def append_observations(self, X_new, Y_new) -> "ExactGP":
+        """Add observations and update the posterior incrementally: the bordered Cholesky of the new
+        rows (GPEngine.append, O(n^2 q)) instead of the full refit the reference runs after appending
+        (optimization/Bayesian.py:163-174 then :89-94 next round; optimization/Bayesian7.py:628-631,639).  Valid
+        because K depends only on the inputs and the (unchanged) hyperparameters; the outcome transform is refitted on
+        all targets and alpha recomputed.  Falls back to ``fit`` (with the jitter schedule) when there is no state yet
+        or the update is not positive definite."""
+        dev = self.train_X.device
+        X_new = torch.as_tensor(X_new, dtype=torch.float64).to(dev)
+        Y_new = torch.as_tensor(Y_new, dtype=torch.float64).to(dev)
+        if Y_new.dim() == 1:
+            Y_new = Y_new.unsqueeze(-1)
+        self.train_X = torch.cat([self.train_X, X_new.reshape(-1, self.train_X.shape[1])])
+        self.train_Y = torch.cat([self.train_Y, Y_new.reshape(-1, self.train_Y.shape[1])])
+        if self.state is None or self.state.n >= self.train_X.shape[0]:
+            return self.fit()
+        Y = self.train_Y
+        if self.outcome_transform is not None:
+            Y = self.outcome_transform.fit(Y).transform(Y)
+        try:
+            self.state = self.engine.append(self.state, self.train_X, Y)
+        except NotPositiveDefiniteError:
+            self.state = None
+            return self.fit()
+        return self
+
     def _untransform(self):
         ot = self.outcome_transform
         if ot is None:

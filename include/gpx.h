@@ -167,6 +167,21 @@ gpx_status gpx_fit_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t
                                int64_t stride_dinv, double* W, int64_t ldw, int64_t stride_w, double* alpha,
                                int64_t stride_alpha, int32_t* info, void* ws, size_t ws_bytes);
 
+/* Incremental posterior update: rows n_old .. n_new-1 of X / Y appended to a GP whose L, Dinv and W
+ * hold a successful fit (gpx_fit_f64 or an earlier append) of the first n_old rows with the SAME kernel parameters.
+ * The reference appends the new observations and refits from scratch every round (optimization/Bayesian7.py:628-631,
+ * 692-700 then :639; optimization/Bayesian.py:163-174); with the hyperparameters unchanged the leading block of the
+ * factor is unchanged, so this bordered update costs O(n^2 q) (q = n_new - n_old) instead of O(n^3) and produces the
+ * factor, W and alpha a fresh gpx_fit_f64 of all n_new rows would (rows past the last full 128-tile of the old fit
+ * are refactored).  L / W must have leading dims >= gpx_padded_n(n_new) (allocate with spare capacity), Dinv room
+ * for 2 * gpx_padded_n(n_new)/64 blocks, alpha gpx_padded_n(n_new) x nrhs.  Y holds all n_new targets (alpha is
+ * recomputed, so a re-standardised Y is fine).  info: device int32, 0 or global failing pivot + 1. */
+gpx_status gpx_append_workspace_size(int64_t n_old, int64_t n_new, int64_t nrhs, size_t* bytes);
+gpx_status gpx_append_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n_old, int64_t n_new, const double* X,
+                          int64_t ldx, const double* Y, int64_t ldy, int64_t nrhs, double* L, int64_t ldl,
+                          double* Dinv, double* W, int64_t ldw, double* alpha, int32_t* info, void* ws,
+                          size_t ws_bytes);
+
 /* ---- posterior / acquisition ---------------------------------------------- */
 /* Posterior at m points Xs (m x d, ld ldxs): mean (m x nrhs, ld ldmean) and variance (m), untransformed
  * by (y_mean[r], y_scale[r]) per output r (host arrays of nrhs; NULL = identity).  Replaces

@@ -23,6 +23,7 @@ What it restates (fp64, NumPy/SciPy):
       the variance-sum pool scan is ``optimization/Bayesian7.py:664-671``).
 * a8  Argmax with the lowest index winning ties (``optimization/Bayesian.py:117``,
       ``optimization/Bayesian7.py:681,724-727``).
+* §8f row 3: the bordered-Cholesky append of new observations (``append``), equal to a refit.
 * §8f row 1: -log p(y) and its gradient w.r.t. the kernel hyperparameters (``mll_value_grad``).
 * a9 / §8f row 2: the batched SVGP predictive of ``optimization/Bayesian7.py:543-563,664-671`` (gpytorch's whitened
       ``VariationalStrategy`` [upstream]: mean = c + k*^T L^{-T} m, var = k** + k*^T L^{-T}(S S^T - I)L^{-1} k* +
@@ -203,6 +204,32 @@ def fit(X: np.ndarray, y: np.ndarray, p: KernelParams) -> GPState:
     L = cholesky(K)
     alpha = sla.cho_solve((L, True), y - p.const_mean, check_finite=False)
     return GPState(X=X, L=L, alpha=alpha, params=p)
+
+
+def append(state: GPState, X_all: np.ndarray, y_all: np.ndarray) -> GPState:
+    """Incremental posterior update: the rows of X_all past ``state.X`` appended by a bordered
+    Cholesky (L21 = K21 L11^{-T}, L22 = chol(K22 - L21 L21^T)) instead of the refit the reference runs every round
+    after appending observations (optimization/Bayesian7.py:628-631,639; optimization/Bayesian.py:163-174).  Equal
+    to ``fit(X_all, y_all, state.params)`` up to rounding; alpha is recomputed from all of y_all."""
+    p = state.params
+    X_all = np.asarray(X_all, dtype=np.float64)
+    y_all = np.asarray(y_all, dtype=np.float64)
+    n0 = state.X.shape[0]
+    Xn = X_all[n0:]
+    K21 = kernel_matrix(Xn, X_all[:n0], p)
+    K22 = gram(Xn, p)
+    L21 = sla.solve_triangular(state.L, K21.T, lower=True, check_finite=False).T
+    try:
+        L22 = cholesky(K22 - L21 @ L21.T)
+    except NotPDError as e:
+        raise NotPDError(n0 + e.pivot) from e
+    n = X_all.shape[0]
+    L = np.zeros((n, n))
+    L[:n0, :n0] = state.L
+    L[n0:, :n0] = L21
+    L[n0:, n0:] = L22
+    alpha = sla.cho_solve((L, True), y_all - p.const_mean, check_finite=False)
+    return GPState(X=X_all, L=L, alpha=alpha, params=p)
 
 
 # ---------------------------------------------------------------------------------------------

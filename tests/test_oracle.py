@@ -165,3 +165,26 @@ def test_golden_fixtures_present():
     names = {os.path.basename(f) for f in FIXTURES}
     assert "real_b6_results256_val512.npz" in names and "real_b7_results256_val512.npz" in names
     assert len(FIXTURES) >= 7
+
+
+@pytest.mark.parametrize("kind", [O.RBF, O.MATERN52, O.SCALE_LINEAR_MATERN52])
+@pytest.mark.parametrize("n_old,q", [(1, 1), (40, 7), (100, 60)])
+def test_append_equals_refit(kind, n_old, q):
+    X, y = O.synthetic_problem(n_old + q, 4, n_old + q)
+    Y = np.stack([y, 2 * y - 1], axis=1)
+    p = params(kind, 4, noise=1e-4, linear_variance=np.full(4, 0.3))
+    st = O.fit(X[:n_old], Y[:n_old], p)
+    app = O.append(st, X, Y)
+    ref = O.fit(X, Y, p)
+    np.testing.assert_allclose(app.L, ref.L, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(app.alpha, ref.alpha, rtol=1e-9, atol=1e-9 * np.abs(ref.alpha).max())
+
+
+def test_append_not_pd_global_pivot():
+    X, y = O.synthetic_problem(30, 3, 1)
+    X = np.vstack([X, [[50.0, 50.0, 50.0]], [[50.0, 50.0, 50.0]]])  # far away: K21 = 0 exactly, then a duplicate
+    p = params(O.RBF, 3, noise=0.0, ls=0.5)
+    st = O.fit(X[:30], y, params(O.RBF, 3, noise=0.0, ls=0.5))
+    with pytest.raises(O.NotPDError) as e:
+        O.append(st, X, np.zeros(32))
+    assert e.value.pivot == 31
