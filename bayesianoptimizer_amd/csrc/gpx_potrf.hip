@@ -231,7 +231,7 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, double* 
 // L_kk from the scratch into A, and D_k = L_kk^{-1} into the first half of Dinv (one workgroup per block).
 __global__ void __launch_bounds__(WG) potrf_dinv_kernel(double* __restrict__ A, int64_t lda, int nblk,
                                                         double* __restrict__ Dinv, const int32_t* __restrict__ info,
-                                                        int64_t sa, int64_t sd) {
+                                                        int64_t sa, int64_t sd, int k0) {
   A += blockIdx.y * sa;
   Dinv += blockIdx.y * sd;
   info += blockIdx.y;
@@ -239,7 +239,7 @@ __global__ void __launch_bounds__(WG) potrf_dinv_kernel(double* __restrict__ A, 
   __shared__ __attribute__((aligned(16))) double sL[NB * LD64];
   __shared__ __attribute__((aligned(16))) double sX[NB * LD64];
   __shared__ __attribute__((aligned(16))) double sT[NB * LD64];
-  const int k = blockIdx.x, t = threadIdx.x;
+  const int k = k0 + (int)blockIdx.x, t = threadIdx.x;
   const double* src = Dinv + (int64_t)(nblk + k) * NB * NB;
   double* Lkk = A + (int64_t)k * NB * lda + (int64_t)k * NB;
 #pragma unroll
@@ -262,13 +262,23 @@ int potrf_step_grid(int c, int nblk) {
   return (nblk - c) + M * (M + 1) / 2;
 }
 
+static void launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
+                         int cbeg, int cend) {
+  for (int c = cbeg; c < cend; ++c)
+    potrf_step_kernel<<<dim3(potrf_step_grid(c, nblk), bt.count), WG, 0, ctx->stream>>>(A, lda, c, nblk, Dinv, info, 0,
+                                                                                         bt.k, bt.dinv);
+}
+
+static void launch_dinv(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
+                        int k0, int k1) {
+  potrf_dinv_kernel<<<dim3(k1 - k0, bt.count), WG, 0, ctx->stream>>>(A, lda, nblk, Dinv, info, bt.k, bt.dinv, k0);
+}
+
 hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt) {
   LaunchTimer tm(ctx, GPX_TIMER_POTRF);
   const int nblk = npad / NB;
-  for (int c = 0; c < nblk; ++c)
-    potrf_step_kernel<<<dim3(potrf_step_grid(c, nblk), bt.count), WG, 0, ctx->stream>>>(A, lda, c, nblk, Dinv, info, 0,
-                                                                                         bt.k, bt.dinv);
-  potrf_dinv_kernel<<<dim3(nblk, bt.count), WG, 0, ctx->stream>>>(A, lda, nblk, Dinv, info, bt.k, bt.dinv);
+  launch_steps(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk);
+  launch_dinv(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk);
   return hipGetLastError();
 }
 

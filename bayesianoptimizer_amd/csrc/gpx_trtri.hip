@@ -32,6 +32,9 @@ __global__ void __launch_bounds__(WG) trtri_diag_kernel(const double* __restrict
 }
 
 // T_p = L21^T W22 for group p of level with half-size h blocks.  blockIdx.z = group + groups * problem.
+// The k-range of tile (rb, cb) is (cb + 1) * 64 (W22 upper), so one workgroup takes the column pair cb and
+// nb2 - 1 - cb: every workgroup then does the same (nb2 + 1) * 64 k-steps (the unpaired form left the long
+// tiles of the last level running alone: 291 us vs the 125 us the level's flops need at the measured MFMA rate).
 __global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ L, int64_t ldl,
                                                      const double* __restrict__ W, int64_t ldw,
                                                      double* __restrict__ T, int h, int nblk, int groups, int64_t sl,
@@ -44,28 +47,33 @@ __global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ 
   T += prob * st;
   const int s1 = p * 2 * h, s2 = s1 + h;
   const int nb2 = min(2 * h, nblk - s1) - h;
-  const int rb = blockIdx.y, cb = blockIdx.x;
-  if (nb2 <= 0 || cb >= nb2) return;
+  const int rb = blockIdx.y;
+  if (nb2 <= 0 || (int)blockIdx.x >= (nb2 + 1) / 2) return;
   const int b1 = h * NB;
   const int64_t off1 = (int64_t)s1 * NB, off2 = (int64_t)s2 * NB;
-  const double* Ab = L + off2 * ldl + off1 + rb * NB;   // A(m=r,k=q) = L[off2+q][off1+r]
-  const double* Bb = W + off2 * ldw + off2 + cb * NB;   // B(k=q,n=c) = W[off2+q][off2+c]
-  Tile tile;
-  tile.run(Ab, ldl, Bb, ldw, 0, (cb + 1) * NB, smem);
   // T_p is b1 x b2 with row length b2; every group before the last is full (b2 = b1), so group p starts at
   // p*b1*b1 and the level's total sum_p b1*b2_p <= b1*(npad-b1) <= npad^2/4 fits the workspace.
   const int b2 = nb2 * NB;
   double* Tp = T + (int64_t)p * b1 * b1;
+  for (int pass = 0; pass < 2; ++pass) {
+    const int cb = pass == 0 ? (int)blockIdx.x : nb2 - 1 - (int)blockIdx.x;
+    if (pass == 1 && cb == (int)blockIdx.x) break;
+    const double* Ab = L + off2 * ldl + off1 + rb * NB;   // A(m=r,k=q) = L[off2+q][off1+r]
+    const double* Bb = W + off2 * ldw + off2 + cb * NB;   // B(k=q,n=c) = W[off2+q][off2+c]
+    Tile tile;
+    tile.run(Ab, ldl, Bb, ldw, 0, (cb + 1) * NB, smem);
 #pragma unroll
-  for (int i = 0; i < Tile::WM; ++i)
+    for (int i = 0; i < Tile::WM; ++i)
 #pragma unroll
-    for (int j = 0; j < Tile::WN; ++j)
+      for (int j = 0; j < Tile::WN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Tp[(int64_t)(rb * NB + Tile::row_of(i, r)) * b2 + cb * NB + Tile::col_of(j)] = tile.acc[i][j][r];
+        for (int r = 0; r < 4; ++r)
+          Tp[(int64_t)(rb * NB + Tile::row_of(i, r)) * b2 + cb * NB + Tile::col_of(j)] = tile.acc[i][j][r];
+  }
 }
 
-// W12 = -W11 T_p
+// W12 = -W11 T_p.  The k-range of tile (rb, cb) is [rb * 64, b1) (W11 upper): one workgroup takes the row pair
+// rb and h - 1 - rb (same balancing as trtri_t_kernel).
 __global__ void __launch_bounds__(WG) trtri_w_kernel(double* __restrict__ W, int64_t ldw, const double* __restrict__ T,
                                                      int h, int nblk, int groups, int64_t sw, int64_t st) {
   using Tile = MfmaTile<NB, NB, 16, false, true>;
@@ -75,23 +83,27 @@ __global__ void __launch_bounds__(WG) trtri_w_kernel(double* __restrict__ W, int
   T += prob * st;
   const int s1 = p * 2 * h, s2 = s1 + h;
   const int nb2 = min(2 * h, nblk - s1) - h;
-  const int rb = blockIdx.y, cb = blockIdx.x;
-  if (nb2 <= 0 || cb >= nb2) return;
+  const int cb = blockIdx.x;
+  if (nb2 <= 0 || cb >= nb2 || (int)blockIdx.y >= (h + 1) / 2) return;
   const int b1 = h * NB;
   const int64_t off1 = (int64_t)s1 * NB, off2 = (int64_t)s2 * NB;
-  const double* Ab = W + (off1 + rb * NB) * ldw + off1;           // A(m=r,k=q) = W[off1+r][off1+q]
   const int b2 = nb2 * NB;
   const double* Bb = T + (int64_t)p * b1 * b1 + cb * NB;          // B(k=q,n=c) = T[q][c], row length b2
-  Tile tile;
-  tile.run(Ab, ldw, Bb, b2, rb * NB, b1, smem);
-  double* Wo = W + (off1 + rb * NB) * ldw + off2 + cb * NB;
+  for (int pass = 0; pass < 2; ++pass) {
+    const int rb = pass == 0 ? (int)blockIdx.y : h - 1 - (int)blockIdx.y;
+    if (pass == 1 && rb == (int)blockIdx.y) break;
+    const double* Ab = W + (off1 + rb * NB) * ldw + off1;           // A(m=r,k=q) = W[off1+r][off1+q]
+    Tile tile;
+    tile.run(Ab, ldw, Bb, b2, rb * NB, b1, smem);
+    double* Wo = W + (off1 + rb * NB) * ldw + off2 + cb * NB;
 #pragma unroll
-  for (int i = 0; i < Tile::WM; ++i)
+    for (int i = 0; i < Tile::WM; ++i)
 #pragma unroll
-    for (int j = 0; j < Tile::WN; ++j)
+      for (int j = 0; j < Tile::WN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        Wo[(int64_t)Tile::row_of(i, r) * ldw + Tile::col_of(j)] = -tile.acc[i][j][r];
+        for (int r = 0; r < 4; ++r)
+          Wo[(int64_t)Tile::row_of(i, r) * ldw + Tile::col_of(j)] = -tile.acc[i][j][r];
+  }
 }
 
 hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, const double* Dinv, double* W,
@@ -101,9 +113,10 @@ hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, cons
   trtri_diag_kernel<<<dim3(nblk, bt.count), WG, 0, c->stream>>>(Dinv, W, ldw, bt.dinv, bt.w);
   for (int h = 1; h < nblk; h *= 2) {
     const int groups = (nblk + 2 * h - 1) / (2 * h);
-    dim3 grid(h, h, groups * bt.count);
-    trtri_t_kernel<<<grid, WG, 0, c->stream>>>(L, ldl, W, ldw, T, h, nblk, groups, bt.k, bt.w, bt.ws);
-    trtri_w_kernel<<<grid, WG, 0, c->stream>>>(W, ldw, T, h, nblk, groups, bt.w, bt.ws);
+    const int hp = (h + 1) / 2;  // paired tiles (load balance, see the kernels)
+    trtri_t_kernel<<<dim3(hp, h, groups * bt.count), WG, 0, c->stream>>>(L, ldl, W, ldw, T, h, nblk, groups, bt.k,
+                                                                         bt.w, bt.ws);
+    trtri_w_kernel<<<dim3(h, hp, groups * bt.count), WG, 0, c->stream>>>(W, ldw, T, h, nblk, groups, bt.w, bt.ws);
   }
   return hipGetLastError();
 }
