@@ -18,6 +18,8 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "gpx.h")
 GPX_MAX_DIM = 32
 GPX_MAX_RHS = 8
 GPX_TILE = 128
+GPX_MAX_Q = 32
+GPX_MAX_GRAD_CANDIDATES = 16384
 
 GPX_OK, GPX_NOT_PD, GPX_INVALID_ARG, GPX_HIP_ERROR, GPX_RCCL_ERROR = 0, 1, 2, 3, 4
 STATUS_NAMES = {0: "OK", 1: "NOT_PD", 2: "INVALID_ARG", 3: "HIP_ERROR", 4: "RCCL_ERROR"}
@@ -103,6 +105,9 @@ _PROTOS = {
     "gpx_append_workspace_size": (c_int32, [c_int64, c_int64, c_int64, POINTER(c_size_t)]),
     "gpx_append_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, c_int64, _p, c_int64, _p, c_int64, c_int64, _p,
                                  c_int64, _p, _p, c_int64, _p, _p, _p, c_size_t]),
+    "gpx_moments_grad_workspace_size": (c_int32, [c_int64, c_int64, POINTER(c_size_t)]),
+    "gpx_moments_grad_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, _p, _p, c_int64,
+                                       c_int64, c_int64, _p, _p, _p, _p, _p, c_size_t]),
     "gpx_sweep_workspace_size": (c_int32, [c_int64, c_int64, c_int64, POINTER(c_size_t)]),
     "gpx_posterior_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, _p, c_int64,
                                     _p, c_int64, c_int64, POINTER(c_double), POINTER(c_double), _p, c_int64, _p,

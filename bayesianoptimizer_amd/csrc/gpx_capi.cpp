@@ -419,6 +419,44 @@ gpx_status gpx_mll_grad_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n,
                                       align256(ws)), "mll");
 }
 
+gpx_status gpx_moments_grad_workspace_size(int64_t n, int64_t m, size_t* bytes) {
+  if (!bytes || n < 1 || m < 1 || m > GPX_MAX_GRAD_CANDIDATES) return GPX_INVALID_ARG;
+  *bytes = gpx::moments_grad_ws_doubles((int)padded(n), (int)m) * sizeof(double) + 256;
+  return GPX_OK;
+}
+
+gpx_status gpx_moments_grad_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                                const double* W, int64_t ldw, const double* alpha, const double* Xs, int64_t m,
+                                int64_t q, int64_t ldxs, double* mean, double* dmean, double* cov, double* dcov,
+                                void* ws, size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_TRY(check_params(c, p));
+  GPX_TRY(check_n(c, n));
+  if (m < 1 || m > GPX_MAX_GRAD_CANDIDATES) return fail(c, GPX_INVALID_ARG, "m must be in [1, GPX_MAX_GRAD_CANDIDATES]");
+  if (q < 1 || q > GPX_MAX_Q || m % q != 0) return fail(c, GPX_INVALID_ARG, "q must be in [1, GPX_MAX_Q] and divide m");
+  GPX_NONNULL(c, X);
+  GPX_NONNULL(c, W);
+  GPX_NONNULL(c, alpha);
+  GPX_NONNULL(c, Xs);
+  GPX_NONNULL(c, mean);
+  GPX_NONNULL(c, dmean);
+  GPX_NONNULL(c, cov);
+  GPX_NONNULL(c, dcov);
+  GPX_NONNULL(c, ws);
+  const int64_t npad = padded(n);
+  GPX_TRY(check_ld(c, ldx, p->d, "X", false));
+  GPX_TRY(check_ld(c, ldw, npad, "W", true));
+  GPX_TRY(check_ld(c, ldxs, p->d, "Xs", false));
+  size_t need = 0;
+  GPX_TRY(gpx_moments_grad_workspace_size(n, m, &need));
+  if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "moments_grad workspace too small");
+  GPX_TRY(use_device(c));
+  return hip_check(c, gpx::launch_moments_grad(c, *p, (int)n, (int)npad, X, ldx, W, ldw, alpha, Xs, ldxs, (int)m,
+                                               (int)q, mean, dmean, cov, dcov, align256(ws)),
+                   "moments_grad");
+}
+
 gpx_status gpx_sweep_workspace_size(int64_t n, int64_t nrhs, int64_t m, size_t* bytes) {
   if (!bytes || n < 1 || m < 1 || nrhs < 1 || nrhs > GPX_MAX_RHS) return GPX_INVALID_ARG;
   *bytes = gpx::sweep_workspace_bytes(padded(n), nrhs, m);

@@ -7,7 +7,7 @@
 namespace gpx {
 
 // k-range of a 64x64 output tile (rb, cb) of C = A B when one operand is upper triangular.
-enum { KR_FULL = 0, KR_B_UPPER = 1, KR_A_UPPER = 2 };
+enum { KR_FULL = 0, KR_B_UPPER = 1, KR_A_UPPER = 2, KR_A_LOWER = 3 };
 
 // Cout(rb, cb) = [Cin(rb, cb)] + sign * sum_k A(m, k) B(k, n) on fp64 MFMA (one 64x64 tile per workgroup).
 //   A_KM: A(m, k) at A[k * lda + m] (else A[m * lda + k]);  B_KM: B(k, n) at B[k * ldb + n] (else B[n * ldb + k]).
@@ -28,6 +28,7 @@ __global__ void __launch_bounds__(WG) gemm64_kernel(const double* __restrict__ A
   int kbeg = 0, kend = K;
   if (KR == KR_B_UPPER) kend = min(K, (cb + 1) * NB);
   if (KR == KR_A_UPPER) kbeg = rb * NB;
+  if (KR == KR_A_LOWER) kend = min(K, (rb + 1) * NB);
   const bool split = gridDim.z > 1;
   if (split) {
     const int k0 = (int)blockIdx.z * kchunk;

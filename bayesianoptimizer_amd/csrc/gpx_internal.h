@@ -104,6 +104,11 @@ hipError_t launch_append(Context* c, const gpx_kernel_params& p, int n_old, int 
                          double* L, int64_t ldl, double* Dinv, double* W, int64_t ldw, int32_t* info, double* ws);
 size_t append_workspace_bytes(int64_t n_old, int64_t n_new);
 
+size_t moments_grad_ws_doubles(int npad, int m);
+hipError_t launch_moments_grad(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
+                               const double* W, int64_t ldw, const double* alpha, const double* Xs, int64_t ldxs,
+                               int m, int q, double* mean, double* dmean, double* cov, double* dcov, double* ws);
+
 size_t mll_workspace_bytes(int64_t npad);
 hipError_t launch_mll(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
                       const double* Y, int64_t ldy, int nrhs, const double* L, int64_t ldl, const double* W,

@@ -437,6 +437,38 @@ class GPEngine:
             return best_val, best_idx, scores
         return best_val, best_idx
 
+    def moments_grad(self, state: GPState, Xs, q: int = 1, alpha: Optional[torch.Tensor] = None):
+        """Posterior mean / q-batch covariance of candidates Xs (m x d, consecutive q-batches) and their derivatives
+        w.r.t. the candidates (gpx_moments_grad_f64), in the engine's standardised units:
+        mean (m), dmean (m x d), cov (m x q: row a of its batch's q x q covariance), dcov (m x d x q, first-argument
+        partials; see include/gpx.h for the chain rule).  ``alpha``: padded_n objective column (default output 0)."""
+        Xs = self._as_f64(Xs, "Xs")
+        m, d = Xs.shape
+        if d != state.d:
+            raise ValueError(f"Xs has {d} columns, model has d={state.d}")
+        if m % q:
+            raise ValueError(f"{m} candidates do not form q-batches of {q}")
+        if alpha is None:
+            alpha = state.alpha[:, 0]
+        alpha = alpha.to(device=self.device, dtype=torch.float64).contiguous()
+        if alpha.numel() != state.npad:
+            raise ValueError("alpha must have padded_n entries")
+        dev = self.device
+        mean = torch.empty((m,), dtype=torch.float64, device=dev)
+        dmean = torch.empty((m, d), dtype=torch.float64, device=dev)
+        cov = torch.empty((m, q), dtype=torch.float64, device=dev)
+        dcov = torch.empty((m, d, q), dtype=torch.float64, device=dev)
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_moments_grad_workspace_size(state.n, m, ctypes.byref(nbytes)))
+        ws = self.workspace("moments_grad", nbytes.value)
+        pc = state.params.to_c(d)
+        self._bind_stream()
+        self._check(self.lib.gpx_moments_grad_f64(
+            self.handle, ctypes.byref(pc), state.n, _ptr(state.X), state.X.stride(0), _ptr(state.W), state.W.stride(0),
+            _ptr(alpha), _ptr(Xs), m, q, Xs.stride(0), _ptr(mean), _ptr(dmean), _ptr(cov), _ptr(dcov), _ptr(ws),
+            ws.numel()))
+        return mean, dmean, cov, dcov
+
     def argmax_combine(self, vals: torch.Tensor, idx: torch.Tensor):
         """Deterministic (max value, lowest index) over device records (after the cross-rank gather)."""
         vals = vals.to(device=self.device, dtype=torch.float64).contiguous().reshape(-1)

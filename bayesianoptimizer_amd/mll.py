@@ -28,6 +28,7 @@ from typing import Callable, List, Optional, Sequence
 
 import numpy as np
 
+from ._capi import GPXError
 from .engine import KernelParams
 
 SQRT2 = math.sqrt(2.0)
@@ -190,7 +191,19 @@ def objective(spec: HyperSpec, value_grad: Callable, n: int):
     def f(raw):
         raw = np.asarray(raw, dtype=np.float64)
         p = spec.params_from_raw(raw)
-        g = value_grad(p)
+        # A line-search trial point outside the parameter domain (a softplus underflowing to 0, an overflow) or a
+        # Gram matrix that stays indefinite through the jitter ladder scores +inf, so L-BFGS-B backtracks (GPyTorch's
+        # NaN loss plays that role in fit_gpytorch_mll_scipy [upstream]).
+        nat = [h.to_natural(float(r)) for h, r in zip(spec.hypers, raw)]
+        if not all(np.isfinite(v) for v in nat) or any(v <= 0.0 for h, v in zip(spec.hypers, nat)
+                                                        if h.name in ("lengthscale", "outputscale", "noise")):
+            return np.inf, np.zeros_like(raw)
+        try:
+            g = value_grad(p)
+        except (GPXError, np.linalg.LinAlgError):
+            return np.inf, np.zeros_like(raw)
+        if not np.isfinite(g["nll"]):
+            return np.inf, np.zeros_like(raw)
         loss = g["nll"]
         grad = np.empty_like(raw)
         for i, (h, r) in enumerate(zip(spec.hypers, raw)):

@@ -9,7 +9,8 @@ What differs, by design: the surrogate is an exact GP on the gpx engine (fp64, o
 8 outputs) instead of the batched SVGP; hyperparameters are fixed (MLL fitting: SURVEY §8f row 1).  Data flow,
 CSV resume, transforms, evaluation metrics, pool-scan acquisition (variance score -> top-K -> farthest-point
 sampling) and the objective/return contract follow Bayesian7.  ``acquisition="logei"|"ei"|"ucb"`` selects the
-analytic improvement sweep of optimization/Bayesian.py:96-113 over a Sobol grid instead.
+analytic improvement sweep of optimization/Bayesian.py:96-113 over a Sobol grid instead, and
+``acquisition="qlogei"`` the reference's optimize_acqf on MC qLogEI (q = batch_size, L-BFGS-B restarts; acqf.py).
 
 Surface mapping (north star fit()/predict()/acquire()):
   fit_gp_model()                 ≙ Bayesian7.fit_gp_model / Bayesian.fit_gp_model
@@ -56,6 +57,12 @@ class GPConfig:
     fit_hyperparameters: bool = True
     prior_set: str = "none"               # "none" (ScaleKernel(Linear + Matern) of Bayesian6/7) | "dim_scaled" | "gamma"
     mll_options: Optional[dict] = None    # scipy L-BFGS-B options
+    # acquisition="qlogei": optimize_acqf settings of optimization/Bayesian.py:100-112
+    mc_samples: int = 512
+    num_restarts: int = 10
+    acqf_raw_samples: int = 1024
+    batch_limit: int = 5
+    maxiter: int = 200
 
 
 class BayesianOptimizer:
@@ -274,6 +281,8 @@ class BayesianOptimizer:
             k_big = max(min(k_big, pool.shape[0]), k)
             _, idx_big = torch.topk(scores, k_big)
             return farthest_point_sampling(pool[idx_big], k, self._rng)
+        if self.acquisition == "qlogei":
+            return self._acquire_qlogei(k)
         grid = torch.tensor(self._sobol(self.config.raw_samples), dtype=self.dtype, device=self.gp_device)
         t = self._objective_alpha()
         # maximise the objective in log-standardised space; "min" mode flips the sign of the incumbent search
@@ -286,6 +295,37 @@ class BayesianOptimizer:
         k = min(k, grid.shape[0])
         _, idx = torch.topk(scores, k)
         return grid[idx]
+
+    def _acquire_qlogei(self, k: int) -> torch.Tensor:
+        """optimize_acqf on MC qLogEI with q = k jointly (optimization/Bayesian.py:96-113: 512 Sobol base samples,
+        num_restarts 10, raw_samples 1024, batch_limit 5, maxiter 200), through the log-input transform, in the
+        log-standardised output space (acqf.py)."""
+        from .acqf import LinearMCObjective, SobolQMCNormalSampler, optimize_acqf, qLogExpectedImprovement
+
+        gp = self.gp_model
+        t = self._objective_alpha()
+        sign = 1.0 if self.objective_mode == "max" else -1.0
+        Ys = self.y_tf(self.train_Y_raw)[:, t]
+        w = [0.0] * gp.num_outputs
+        w[t] = sign
+        seed = int(self._rng.integers(0, 1 << 30))
+        acq = qLogExpectedImprovement(gp, best_f=float((sign * Ys).max()),
+                                      sampler=SobolQMCNormalSampler(torch.Size([self.config.mc_samples]), seed),
+                                      objective=LinearMCObjective(w))
+        x_tf = self.x_tf
+
+        class _OnUnitCube:  # the GP sees transformed inputs; optimize_acqf works in the unit cube
+            model = gp
+
+            def __call__(self, X):
+                return acq(x_tf(X.reshape(-1, X.shape[-1])).reshape(X.shape))
+
+        bounds = torch.stack([torch.zeros(self.dim), torch.ones(self.dim)]).to(self.dtype)
+        cand, _ = optimize_acqf(_OnUnitCube(), bounds, q=k, num_restarts=self.config.num_restarts,
+                                raw_samples=self.config.acqf_raw_samples,
+                                options={"batch_limit": self.config.batch_limit, "maxiter": self.config.maxiter},
+                                seed=seed)
+        return cand.detach()
 
     def optimize_acquisition_function(self, gp=None) -> torch.Tensor:
         return self.acquire(self.batch_size)

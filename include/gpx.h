@@ -33,6 +33,8 @@ extern "C" {
 #define GPX_MAX_DIM 32
 #define GPX_MAX_RHS 8
 #define GPX_TILE 128
+#define GPX_MAX_Q 32                    /* q-batch size of gpx_moments_grad_f64 */
+#define GPX_MAX_GRAD_CANDIDATES 16384  /* candidates per gpx_moments_grad_f64 call */
 
 typedef struct gpx_context* gpx_handle;
 typedef int32_t gpx_status;
@@ -209,6 +211,23 @@ gpx_status gpx_acquire_argmax_f64(gpx_handle h, const gpx_kernel_params* p, int6
  * never wins.  Used after the cross-GPU all-gather of per-rank records. */
 gpx_status gpx_argmax_combine_f64(gpx_handle h, const double* vals, const int64_t* idx, int64_t count,
                                   double* best_val, int64_t* best_idx);
+
+/* ---- gradients for acquisition optimisation ---------------------------------------------- */
+/* Posterior moments of m candidates Xs (m x d) grouped in consecutive q-batches (m/q batches of q points: restarts of
+ * optimize_acqf x its q, optimization/Bayesian.py:105-112, optimization/Bayesian2.py:240-245) and their derivatives
+ * w.r.t. the candidates, for the L-BFGS-B refinement that BoTorch drives with torch autograd [upstream].  In the
+ * engine's (standardised) units, with alpha one padded_n column and c ranging over a's batch:
+ *   mean[a]   = const_mean + k_a^T alpha                 dmean[a*d + j]       = d mean[a] / d x_aj
+ *   cov[a*q + c'] = k(x_a, x_c) - k_a^T K^{-1} k_c     dcov[(a*d + j)*q + c'] = d1 k(x_a, x_c)/dx_aj - d k_a/dx_aj^T K^{-1} k_c
+ * (c = batch start + c'; d1 = derivative in the first argument only, so that the gradient of a function L of the batch
+ * covariance is dL/dx_aj = sum_c' (G[a][c] + G[c][a]) dcov[(a*d+j)*q + c'] with G = dL/dcov).  K^{-1} k_c = W (W^T k_c)
+ * on fp64 MFMA; the q-batch posterior covariance is noise-free (add noise for observation noise).  All outputs are
+ * device arrays; deterministic. */
+gpx_status gpx_moments_grad_workspace_size(int64_t n, int64_t m, size_t* bytes);
+gpx_status gpx_moments_grad_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                                const double* W, int64_t ldw, const double* alpha, const double* Xs, int64_t m,
+                                int64_t q, int64_t ldxs, double* mean, double* dmean, double* cov, double* dcov,
+                                void* ws, size_t ws_bytes);
 
 /* ---- marginal likelihood -------------------------------------------------------- */
 /* Negative log marginal likelihood of a fitted exact GP with T = nrhs outputs sharing the covariance (T = 1:

@@ -24,6 +24,8 @@ What it restates (fp64, NumPy/SciPy):
 * a8  Argmax with the lowest index winning ties (``optimization/Bayesian.py:117``,
       ``optimization/Bayesian7.py:681,724-727``).
 * §8f row 3: the bordered-Cholesky append of new observations (``append``), equal to a refit.
+* §8f row 4: q-batch posterior moments and their candidate gradients (``moments_grad``) and the MC qLogEI of
+      the optimize_acqf refinement (``qlogei``), optimization/Bayesian.py:96-113.
 * §8f row 1: -log p(y) and its gradient w.r.t. the kernel hyperparameters (``mll_value_grad``).
 * a9 / §8f row 2: the batched SVGP predictive of ``optimization/Bayesian7.py:543-563,664-671`` (gpytorch's whitened
       ``VariationalStrategy`` [upstream]: mean = c + k*^T L^{-T} m, var = k** + k*^T L^{-T}(S S^T - I)L^{-1} k* +
@@ -374,6 +376,75 @@ def acquisition(mu, var, kind: int, best_f: float = 0.0, beta: float = 4.0):
     if kind == ACQ_VARIANCE:
         return var
     raise ValueError(f"unknown acquisition {kind}")
+
+
+# ---------------------------------------------------------------------------------------------
+# §8f row 4: q-batch posterior moments, their candidate gradients, MC qLogEI (optimize_acqf refinement,
+# optimization/Bayesian.py:96-113, optimization/Bayesian2.py:218-245; BoTorch/GPyTorch autograd [upstream])
+# ---------------------------------------------------------------------------------------------
+def kernel_grad_first(Xa: np.ndarray, Xb: np.ndarray, p: KernelParams) -> np.ndarray:
+    """d k(a, b) / d a_j for every pair: (na, nb, d)."""
+    ls = np.asarray(p.lengthscale, dtype=np.float64)
+    diff = (Xa[:, None, :] / ls - Xb[None, :, :] / ls) / ls  # (a_j - b_j) / l_j^2
+    r2 = _sqdist_scaled(Xa, Xb, ls)
+    if p.kind == RBF:
+        coef = -p.outputscale * np.exp(-0.5 * r2)
+    else:
+        r = np.sqrt(r2)
+        coef = -p.outputscale * (5.0 / 3.0) * (1.0 + math.sqrt(5.0) * r) * np.exp(-math.sqrt(5.0) * r)
+    g = coef[:, :, None] * diff
+    if p.kind == SCALE_LINEAR_MATERN52:
+        g = g + p.outputscale * (np.asarray(p.linear_variance)[None, None, :] * Xb[None, :, :])
+    return g
+
+
+def moments_grad(state: GPState, Xs: np.ndarray, q: int, alpha: Optional[np.ndarray] = None):
+    """NumPy restatement of gpx_moments_grad_f64: mean (m), dmean (m, d), cov (m, q), dcov (m, d, q)."""
+    p = state.params
+    alpha = state.alpha if alpha is None else alpha
+    alpha = alpha[:, 0] if alpha.ndim == 2 else alpha
+    m, d = Xs.shape
+    Ks = kernel_matrix(state.X, Xs, p)  # (n, m)
+    S = sla.cho_solve((state.L, True), Ks, check_finite=False)  # K^{-1} K*
+    G = kernel_grad_first(Xs, state.X, p)  # (m, n, d)
+    mean = p.const_mean + Ks.T @ alpha
+    dmean = np.einsum("anj,n->aj", G, alpha)
+    cov = np.empty((m, q))
+    dcov = np.empty((m, d, q))
+    for a in range(m):
+        b0 = (a // q) * q
+        cols = slice(b0, b0 + q)
+        kp = kernel_matrix(Xs[a:a + 1], Xs[cols], p)[0]
+        gp = kernel_grad_first(Xs[a:a + 1], Xs[cols], p)[0]  # (q, d)
+        cov[a] = kp - Ks[:, a] @ S[:, cols]
+        dcov[a] = gp.T - G[a].T @ S[:, cols]
+    return mean, dmean, cov, dcov
+
+
+def sobol_normal_base_samples(S: int, q: int, seed: int) -> np.ndarray:
+    """The base samples of the product's SobolQMCNormalSampler (torch SobolEngine, scramble, seed; inverse cdf)."""
+    import torch
+    u = torch.quasirandom.SobolEngine(dimension=q, scramble=True, seed=seed).draw(S, dtype=torch.float64).numpy()
+    eps = np.finfo(np.float64).eps
+    v = 0.5 + (1.0 - eps) * (u - 0.5)
+    from scipy.special import erfinv
+    return erfinv(2.0 * v - 1.0) * math.sqrt(2.0)
+
+
+def qlogei(mu: np.ndarray, Sigma: np.ndarray, z: np.ndarray, best_f: float, fat: bool = True,
+           tau_max: float = 1e-2, tau_relu: float = 1e-6) -> np.ndarray:
+    """MC qLogEI of q-batches: mu (B, q), Sigma (B, q, q), base samples z (S, q) -> (B,)."""
+    from scipy.special import logsumexp
+    L = np.linalg.cholesky(0.5 * (Sigma + np.swapaxes(Sigma, 1, 2)))
+    f = mu[None] + np.einsum("bij,sj->sbi", L, z)
+    y = (f - best_f) / tau_relu
+    if fat:
+        sp = np.logaddexp(0.0, y)
+        li = math.log(tau_relu) + np.log(sp + 0.1 / (1.0 + y * y))
+    else:
+        li = math.log(tau_relu) + np.where(y > -37.0, np.log(np.logaddexp(0.0, np.maximum(y, -37.0))), y)
+    qred = tau_max * logsumexp(li / tau_max, axis=-1)
+    return logsumexp(qred, axis=0) - math.log(z.shape[0])
 
 
 # ---------------------------------------------------------------------------------------------

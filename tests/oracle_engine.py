@@ -88,6 +88,13 @@ class OracleEngine:
         out = (torch.tensor([v]), torch.tensor([i + index_offset]))
         return out + (torch.tensor(scores),) if return_scores else out
 
+    def moments_grad(self, state, Xs, q=1, alpha=None):
+        self.calls["moments_grad"] = self.calls.get("moments_grad", 0) + 1
+        Xs = torch.as_tensor(Xs, dtype=torch.float64).cpu().numpy()
+        a = state.alpha[:, 0] if alpha is None else torch.as_tensor(alpha)
+        out = O.moments_grad(state.st, Xs, q, a.cpu().numpy()[: state.n])
+        return tuple(torch.tensor(v) for v in out)
+
     def argmax_combine(self, vals, idx):
         v, i = O.combine_argmax(list(zip(vals.tolist(), idx.tolist())))
         return torch.tensor([v]), torch.tensor([i])

@@ -131,6 +131,18 @@ def test_dropin_optimizer_driven_like_run_optimization(tmp_path, acq):
     assert best_value == pytest.approx(data[:40, 5:].sum(1).min(), rel=1e-6)
 
 
+def test_dropin_optimizer_qlogei_mode(tmp_path):
+    # acquisition="qlogei": optimize_acqf on MC qLogEI with q = batch_size (Bayesian.py:96-113), small settings
+    cfg = GPConfig(mc_samples=64, num_restarts=2, acqf_raw_samples=32, batch_limit=2, maxiter=5,
+                   fit_hyperparameters=False)
+    best_params, _ = run_optimization_like(BayesianOptimizer, total_evaluations=20, n_initial_points=16, batch_size=2,
+                                           output_dir=str(tmp_path / "q"), engine=OracleEngine(), gp_config=cfg,
+                                           acquisition="qlogei", seed=0)
+    assert best_params.shape == (5,)
+    lines = open(tmp_path / "q" / "optimization_results.csv").read().strip().splitlines()
+    assert len(lines) - 1 == 20
+
+
 def test_dropin_predict_matches_oracle(tmp_path):
     sim = StubSimulator()
     opt = BayesianOptimizer(sim, BOUNDS, str(tmp_path), n_initial_points=30, n_batches=0, batch_size=4,
