@@ -25,6 +25,7 @@
 #include "gpx_internal.h"
 #include "gpx_device.h"
 #include "gpx_chol64.h"
+#include <cstdlib>
 
 // Optional timestamp hook for tools/potrf_bench.hip (compiled out in the library).
 #ifndef GPX_PANEL_STAMP
@@ -74,7 +75,7 @@ __device__ __forceinline__ void load_tile_lds(const double* __restrict__ G, int6
 }
 
 // Panel workgroup p of block column c (see the file comment).
-__device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, int c, int p, int nblk,
+__device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, int c, int p, int nblk, int lazy,
                                            double* __restrict__ Dinv, int32_t* __restrict__ info, double* lds) {
   double* sA = lds;             // A_cc -> L_cc
   double* sP = sA + NB * LD64;  // A_ic -> L_ic (p > 0)
@@ -89,14 +90,25 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
   double* Aic = A + (int64_t)bi * NB * lda + (int64_t)c * NB;
   if (t == 0) s_tdone = 0;
   if (c > 0) {
-    // step-(c-1) update of the two tiles this workgroup factors
-    const double* Lc = A + (int64_t)c * NB * lda + (int64_t)(c - 1) * NB;
+    // the updates of block columns c0 .. c-1 not yet applied by a trailing flush, on the two tiles this workgroup
+    // factors (K = 64 (c - c0) <= 64 lazy)
+    const int c0 = lazy * ((c - 1) / lazy);
+    const int kk = (c - c0) * NB;
+    const double* Lc = A + (int64_t)c * NB * lda + (int64_t)c0 * NB;
     Tile64 tl;
-    tl.run(Lc, lda, Lc, lda, 0, NB, smem);
+    // K = 64 (the eager case, on the critical path of every step) with a compile-time trip count
+    if (kk == NB)
+      tl.run(Lc, lda, Lc, lda, 0, NB, smem);
+    else
+      tl.run(Lc, lda, Lc, lda, 0, kk, smem);
     tile_sub_to_lds(tl, Acc, lda, sA);
     if (panel) {
       __syncthreads();  // smem reuse
-      tl.run(A + (int64_t)bi * NB * lda + (int64_t)(c - 1) * NB, lda, Lc, lda, 0, NB, smem);
+      const double* Li = A + (int64_t)bi * NB * lda + (int64_t)c0 * NB;
+      if (kk == NB)
+        tl.run(Li, lda, Lc, lda, 0, NB, smem);
+      else
+        tl.run(Li, lda, Lc, lda, 0, kk, smem);
       // run() ends with a barrier after its last LDS read, so the epilogue may overwrite the staging (sP)
       tile_sub_to_lds(tl, Aic, lda, sP);
     }
@@ -178,21 +190,23 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
   }
 }
 
-// Trailing workgroup: 128x128 tile `tile` of the lower triangle of block columns >= c+1, A_ij -= L_{i,c-1} L_{j,c-1}^T.
-// The 128-grid is aligned to the end of the matrix (first 64-block c0 = nblk - 2M); when it starts at block c, that
-// block row/column is computed but not stored (it belongs to this launch's panel).
-__device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t lda, int c, int nblk, int tile, double* lds) {
+// Trailing workgroup of a flush launch c (c % lazy == 0): 128x128 tile `tile` of the lower triangle of block columns
+// >= c+1, A_ij -= sum_{k = c-lazy}^{c-1} L_ik L_jk^T (K = 64 lazy).  The 128-grid is aligned to the end of the matrix
+// (first 64-block c0 = nblk - 2M); when it starts at block c, that block row/column is computed but not stored (it
+// belongs to this launch's panel).
+__device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t lda, int c, int nblk, int lazy, int tile,
+                                              double* lds) {
   const int m = nblk - c - 1;
   const int M = (m + 1) / 2;
   const int c0 = nblk - 2 * M;
   int I, J;
   tri_decode(tile, I, J);
   const int r0 = c0 + 2 * I, q0 = c0 + 2 * J;
-  const double* Li = A + (int64_t)r0 * NB * lda + (int64_t)(c - 1) * NB;
-  const double* Lj = A + (int64_t)q0 * NB * lda + (int64_t)(c - 1) * NB;
+  const double* Li = A + (int64_t)r0 * NB * lda + (int64_t)(c - lazy) * NB;
+  const double* Lj = A + (int64_t)q0 * NB * lda + (int64_t)(c - lazy) * NB;
   double* C = A + (int64_t)r0 * NB * lda + (int64_t)q0 * NB;
   Tile128 tl;
-  tl.run(Li, lda, Lj, lda, 0, NB, lds);
+  tl.run(Li, lda, Lj, lda, 0, lazy * NB, lds);
   // C - acc, stored for the 64-blocks (rb, cb) with cb >= c+1 and rb >= cb; loads of a row group first
 #pragma unroll
   for (int i = 0; i < Tile128::WM; ++i) {
@@ -213,7 +227,7 @@ __device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t ld
 }
 
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
-potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, double* __restrict__ Dinv,
+potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, int lazy, double* __restrict__ Dinv,
                   int32_t* __restrict__ info, int first_wg, int64_t sa, int64_t sd) {
   A += blockIdx.y * sa;  // problem of a batched fit
   Dinv += blockIdx.y * sd;
@@ -223,9 +237,9 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, double* 
   const int npanel = nblk - c;
   const int b = first_wg + (int)blockIdx.x;
   if (b < npanel)
-    panel_role(A, lda, c, b, nblk, Dinv, info, lds);
+    panel_role(A, lda, c, b, nblk, lazy, Dinv, info, lds);
   else
-    trailing_role(A, lda, c, nblk, b - npanel, lds);
+    trailing_role(A, lda, c, nblk, lazy, b - npanel, lds);
 }
 
 // L_kk from the scratch into A, and D_k = L_kk^{-1} into the first half of Dinv (one workgroup per block).
@@ -256,17 +270,35 @@ __global__ void __launch_bounds__(WG) potrf_dinv_kernel(double* __restrict__ A, 
   for (int e = t; e < NB * NB; e += WG) D[e] = sX[(e >> 6) * LD64 + (e & 63)];
 }
 
-int potrf_step_grid(int c, int nblk) {
+// Trailing updates are flushed every `lazy` launches (K = 64 lazy per flush): C tiles are read and written once per
+// `lazy` block columns instead of every column, and the panel workgroups apply the (at most `lazy`) pending columns
+// to their own tiles.
+// Measured (tools/lazy_sweep.sh, profiles/r01_potrf_lazy_sweep.log): n = 4096: lazy 1/2 -> potrf 1.73/1.90 ms (the
+// K = 128 panel pre-update sits on the critical path, the trailing update mostly hides under the panel chain);
+// n = 8192: lazy 1/2/4 -> 7.05/6.75/7.21 ms; n = 16384: lazy 1/2/4/8 -> 46.3/37.4/34.3/35.3 ms (the trailing update
+// dominates).  GPX_POTRF_LAZY overrides.
+static int potrf_lazy(int nblk) {
+  static const int env = [] {
+    const char* e = std::getenv("GPX_POTRF_LAZY");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (env > 0) return env > 8 ? 8 : env;
+  return nblk > 128 ? 4 : (nblk > 64 ? 2 : 1);
+}
+
+int potrf_step_grid(int c, int nblk, int lazy) {
   const int m = nblk - c - 1;
-  const int M = (c > 0 && m > 0) ? (m + 1) / 2 : 0;  // launch 0 has no trailing update
+  const bool flush = c >= lazy && c % lazy == 0;
+  const int M = (flush && m > 0) ? (m + 1) / 2 : 0;
   return (nblk - c) + M * (M + 1) / 2;
 }
 
 static void launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
                          int cbeg, int cend) {
+  const int lazy = potrf_lazy(nblk);
   for (int c = cbeg; c < cend; ++c)
-    potrf_step_kernel<<<dim3(potrf_step_grid(c, nblk), bt.count), WG, 0, ctx->stream>>>(A, lda, c, nblk, Dinv, info, 0,
-                                                                                         bt.k, bt.dinv);
+    potrf_step_kernel<<<dim3(potrf_step_grid(c, nblk, lazy), bt.count), WG, 0, ctx->stream>>>(
+        A, lda, c, nblk, lazy, Dinv, info, 0, bt.k, bt.dinv);
 }
 
 static void launch_dinv(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,

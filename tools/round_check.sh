@@ -1,0 +1,9 @@
+# Full GPU check of the tree: parity suite, smoke, bench (N=1, P=1 and P=4), rocprofv3 kernel stats of the bench.
+set -o pipefail
+mkdir -p gpurun_out/prof
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 &&
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
+timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err &&
+timeout -k 10 300 python bench.py --problems-per-gpu 4 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_p4.json 2> gpurun_out/bench_p4.err &&
+cd /tmp && export TMPDIR=/tmp &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o bench -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof_bench.json 2> $GRAFT_REPO_ROOT/gpurun_out/prof_bench.err
