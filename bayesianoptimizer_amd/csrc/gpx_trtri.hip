@@ -31,15 +31,17 @@ __global__ void __launch_bounds__(WG) trtri_diag_kernel(const double* __restrict
   }
 }
 
-// T_p = L21^T W22 for group p of level with half-size h blocks.  blockIdx.z = group + groups * problem.
-// The k-range of tile (rb, cb) is (cb + 1) * 64 (W22 upper), so one workgroup takes the column pair cb and
-// nb2 - 1 - cb: every workgroup then does the same (nb2 + 1) * 64 k-steps (the unpaired form left the long
-// tiles of the last level running alone: 291 us vs the 125 us the level's flops need at the measured MFMA rate).
+// T_p = L21^T W22 for group p of level with half-size h blocks (TS x TS output tiles; TS = 64, or 128 for the big
+// levels of large n).  blockIdx.z = group + groups * problem.  The k-range of tile (rb, cb) is (cb + 1) * TS (W22
+// upper; its 128-aligned diagonal tiles have the strictly-lower 64-block zeroed by trtri_diag), so one workgroup
+// takes the column pair cb and nt2 - 1 - cb: every workgroup then does the same (nt2 + 1) * TS k-steps (the
+// unpaired form left the long tiles of the last level running alone: 291 us vs 176 us at n = 4096).
+template <int TS>
 __global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ L, int64_t ldl,
                                                      const double* __restrict__ W, int64_t ldw,
                                                      double* __restrict__ T, int h, int nblk, int groups, int64_t sl,
                                                      int64_t sw, int64_t st) {
-  using Tile = MfmaTile<NB, NB, 16, true, true>;
+  using Tile = MfmaTile<TS, TS, 16, true, true>;
   __shared__ __attribute__((aligned(16))) double smem[Tile::LDS_DOUBLES];
   const int p = blockIdx.z % groups, prob = blockIdx.z / groups;
   L += prob * sl;
@@ -47,55 +49,56 @@ __global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ 
   T += prob * st;
   const int s1 = p * 2 * h, s2 = s1 + h;
   const int nb2 = min(2 * h, nblk - s1) - h;
+  const int b1 = h * NB, b2 = nb2 * NB;
+  const int nt2 = b2 / TS;
   const int rb = blockIdx.y;
-  if (nb2 <= 0 || (int)blockIdx.x >= (nb2 + 1) / 2) return;
-  const int b1 = h * NB;
+  if (nb2 <= 0 || (int)blockIdx.x >= (nt2 + 1) / 2) return;
   const int64_t off1 = (int64_t)s1 * NB, off2 = (int64_t)s2 * NB;
   // T_p is b1 x b2 with row length b2; every group before the last is full (b2 = b1), so group p starts at
   // p*b1*b1 and the level's total sum_p b1*b2_p <= b1*(npad-b1) <= npad^2/4 fits the workspace.
-  const int b2 = nb2 * NB;
   double* Tp = T + (int64_t)p * b1 * b1;
   for (int pass = 0; pass < 2; ++pass) {
-    const int cb = pass == 0 ? (int)blockIdx.x : nb2 - 1 - (int)blockIdx.x;
+    const int cb = pass == 0 ? (int)blockIdx.x : nt2 - 1 - (int)blockIdx.x;
     if (pass == 1 && cb == (int)blockIdx.x) break;
-    const double* Ab = L + off2 * ldl + off1 + rb * NB;   // A(m=r,k=q) = L[off2+q][off1+r]
-    const double* Bb = W + off2 * ldw + off2 + cb * NB;   // B(k=q,n=c) = W[off2+q][off2+c]
+    const double* Ab = L + off2 * ldl + off1 + rb * TS;   // A(m=r,k=q) = L[off2+q][off1+r]
+    const double* Bb = W + off2 * ldw + off2 + cb * TS;   // B(k=q,n=c) = W[off2+q][off2+c]
     Tile tile;
-    tile.run(Ab, ldl, Bb, ldw, 0, (cb + 1) * NB, smem);
+    tile.run(Ab, ldl, Bb, ldw, 0, (cb + 1) * TS, smem);
 #pragma unroll
     for (int i = 0; i < Tile::WM; ++i)
 #pragma unroll
       for (int j = 0; j < Tile::WN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          Tp[(int64_t)(rb * NB + Tile::row_of(i, r)) * b2 + cb * NB + Tile::col_of(j)] = tile.acc[i][j][r];
+          Tp[(int64_t)(rb * TS + Tile::row_of(i, r)) * b2 + cb * TS + Tile::col_of(j)] = tile.acc[i][j][r];
   }
 }
 
-// W12 = -W11 T_p.  The k-range of tile (rb, cb) is [rb * 64, b1) (W11 upper): one workgroup takes the row pair
-// rb and h - 1 - rb (same balancing as trtri_t_kernel).
+// W12 = -W11 T_p.  The k-range of tile (rb, cb) is [rb * TS, b1) (W11 upper): one workgroup takes the row pair
+// rb and nt1 - 1 - rb (same balancing as trtri_t_kernel).
+template <int TS>
 __global__ void __launch_bounds__(WG) trtri_w_kernel(double* __restrict__ W, int64_t ldw, const double* __restrict__ T,
                                                      int h, int nblk, int groups, int64_t sw, int64_t st) {
-  using Tile = MfmaTile<NB, NB, 16, false, true>;
+  using Tile = MfmaTile<TS, TS, 16, false, true>;
   __shared__ __attribute__((aligned(16))) double smem[Tile::LDS_DOUBLES];
   const int p = blockIdx.z % groups, prob = blockIdx.z / groups;
   W += prob * sw;
   T += prob * st;
   const int s1 = p * 2 * h, s2 = s1 + h;
   const int nb2 = min(2 * h, nblk - s1) - h;
+  const int b1 = h * NB, b2 = nb2 * NB;
+  const int nt1 = b1 / TS, nt2 = b2 / TS;
   const int cb = blockIdx.x;
-  if (nb2 <= 0 || cb >= nb2 || (int)blockIdx.y >= (h + 1) / 2) return;
-  const int b1 = h * NB;
+  if (nb2 <= 0 || cb >= nt2 || (int)blockIdx.y >= (nt1 + 1) / 2) return;
   const int64_t off1 = (int64_t)s1 * NB, off2 = (int64_t)s2 * NB;
-  const int b2 = nb2 * NB;
-  const double* Bb = T + (int64_t)p * b1 * b1 + cb * NB;          // B(k=q,n=c) = T[q][c], row length b2
+  const double* Bb = T + (int64_t)p * b1 * b1 + cb * TS;          // B(k=q,n=c) = T[q][c], row length b2
   for (int pass = 0; pass < 2; ++pass) {
-    const int rb = pass == 0 ? (int)blockIdx.y : h - 1 - (int)blockIdx.y;
+    const int rb = pass == 0 ? (int)blockIdx.y : nt1 - 1 - (int)blockIdx.y;
     if (pass == 1 && rb == (int)blockIdx.y) break;
-    const double* Ab = W + (off1 + rb * NB) * ldw + off1;           // A(m=r,k=q) = W[off1+r][off1+q]
+    const double* Ab = W + (off1 + rb * TS) * ldw + off1;           // A(m=r,k=q) = W[off1+r][off1+q]
     Tile tile;
-    tile.run(Ab, ldw, Bb, b2, rb * NB, b1, smem);
-    double* Wo = W + (off1 + rb * NB) * ldw + off2 + cb * NB;
+    tile.run(Ab, ldw, Bb, b2, rb * TS, b1, smem);
+    double* Wo = W + (off1 + rb * TS) * ldw + off2 + cb * TS;
 #pragma unroll
     for (int i = 0; i < Tile::WM; ++i)
 #pragma unroll
@@ -113,10 +116,21 @@ hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, cons
   trtri_diag_kernel<<<dim3(nblk, bt.count), WG, 0, c->stream>>>(Dinv, W, ldw, bt.dinv, bt.w);
   for (int h = 1; h < nblk; h *= 2) {
     const int groups = (nblk + 2 * h - 1) / (2 * h);
+    // 128x128 tiles (half the operand traffic per flop) once a level still fills the chip with them: >= 512 paired
+    // workgroups per problem (n = 16384: levels h >= 32; n = 8192: the last level; n <= 4096: never).  Decided per
+    // problem size, not batch count, so a batched fit stays bit-identical to single fits.
+    const int h128 = h / 2;
+    if (h >= 2 && (int64_t)groups * h128 * ((h128 + 1) / 2) >= 512) {
+      trtri_t_kernel<128><<<dim3((h128 + 1) / 2, h128, groups * bt.count), WG, 0, c->stream>>>(
+          L, ldl, W, ldw, T, h, nblk, groups, bt.k, bt.w, bt.ws);
+      trtri_w_kernel<128><<<dim3(h128, (h128 + 1) / 2, groups * bt.count), WG, 0, c->stream>>>(W, ldw, T, h, nblk,
+                                                                                                groups, bt.w, bt.ws);
+      continue;
+    }
     const int hp = (h + 1) / 2;  // paired tiles (load balance, see the kernels)
-    trtri_t_kernel<<<dim3(hp, h, groups * bt.count), WG, 0, c->stream>>>(L, ldl, W, ldw, T, h, nblk, groups, bt.k,
-                                                                         bt.w, bt.ws);
-    trtri_w_kernel<<<dim3(h, hp, groups * bt.count), WG, 0, c->stream>>>(W, ldw, T, h, nblk, groups, bt.w, bt.ws);
+    trtri_t_kernel<NB><<<dim3(hp, h, groups * bt.count), WG, 0, c->stream>>>(L, ldl, W, ldw, T, h, nblk, groups,
+                                                                             bt.k, bt.w, bt.ws);
+    trtri_w_kernel<NB><<<dim3(h, hp, groups * bt.count), WG, 0, c->stream>>>(W, ldw, T, h, nblk, groups, bt.w, bt.ws);
   }
   return hipGetLastError();
 }

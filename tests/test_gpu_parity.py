@@ -420,3 +420,27 @@ def test_fit_batched_reports_not_pd_per_problem(engine):
     assert [st.pivot_failure() for st in sts] == [-1, 1, -1]
     with pytest.raises(NotPositiveDefiniteError):
         engine.fit_batched(t(Xs), t(np.zeros((B, n))), kp)
+
+
+@pytest.mark.parametrize("n,kind", [(8192, "rbf"), (16384, "matern52")])
+def test_large_fit_inverse_and_factor_rows(engine, n, kind):
+    # sizes whose TRTRI uses the 128x128-tile levels and whose Cholesky uses the lazy trailing flush
+    d = 8
+    X, y = O.synthetic_problem(n, d, 1)
+    kp, op = pair(kind, d, noise=1e-4)
+    st = engine.fit(t(X), t(y), kp)
+    rows = np.sort(np.random.default_rng(n).choice(n, 16, replace=False))
+    ri = torch.tensor(rows, device=DEV)
+    Lt = torch.tril(st.L[:n, :n])
+    # (L L^T)[rows] = K[rows]
+    Kr = O.kernel_matrix(X[rows], X, op)
+    Kr[np.arange(16), rows] += op.noise
+    assert np.abs((Lt[ri] @ Lt.T).cpu().numpy() - Kr).max() <= 1e-11
+    # (L^{-1} L)[rows] = I[rows] with L^{-1} = W^T
+    prod = torch.triu(st.W[:n, :n]).T[ri] @ Lt
+    eye = torch.zeros_like(prod)
+    eye[torch.arange(16, device=DEV), ri] = 1.0
+    assert (prod - eye).abs().max().item() <= 1e-9
+    ost_rows = O.sobol_candidates(64, d, 3)
+    mu, var = engine.posterior(st, t(ost_rows))
+    assert torch.isfinite(mu).all() and bool((var > 0).all())
