@@ -60,16 +60,36 @@ __device__ __forceinline__ double bpermute_f64(int src_lane, double v) {
   return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
+// Lane (r + 16 G) of every 16-lane row position r, broadcast to all four rows of the wave: gfx950's
+// v_permlane32_swap (rows 2,3 <-> rows 0,1 of a second copy) then v_permlane16_swap (odd <-> even rows), two VALU
+// ops per 32-bit half instead of a ds_bpermute round trip through the LDS crossbar on the pivot chain.
+template <int G>
+__device__ __forceinline__ unsigned xrow_bcast_u32(unsigned x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);  // [0]: rows (0 1 0 1), [1]: rows (2 3 2 3)
+  const unsigned y = (G < 2) ? r[0] : r[1];
+  const auto s = __builtin_amdgcn_permlane16_swap(y, y, false, false);  // [0]: even row everywhere, [1]: odd row
+  return (G % 2 == 0) ? s[0] : s[1];
+}
+
+template <int G>
+__device__ __forceinline__ double xrow_bcast_f64(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = xrow_bcast_u32<G>((unsigned)(u & 0xffffffffull));
+  const unsigned hi = xrow_bcast_u32<G>((unsigned)(u >> 32));
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
 // Pivot J of the 16x16 block: rows r > J get A[r][c] -= A[r][J] A[J][c] / A[J][J], row J of X is scaled by
 // A[J][J]^{-1/2} and X's rows r > J get the same row operation; rows < J are left untouched.  Row J of A and of X
 // (the lane's own four columns) come from lane J of the same 16-lane DPP row (row_newbcast:J); A[r][J] lives in DPP
-// row J/4 and comes by ds_bpermute.  Measured per pivot: 306 cycles with 64-bit DPP moves, 390 with a wave-local
-// LDS broadcast slot (two ds_read_b128 per row, a write -> read round trip on the chain).
+// row J/4 and comes by two permlane swaps (xrow_bcast_f64).  Measured per pivot: 306 cycles with 64-bit DPP moves,
+// 390 with a wave-local LDS broadcast slot (two ds_read_b128 per row, a write -> read round trip on the chain), ~380
+// with ds_bpermute for A[r][J].
 template <int J>
 __device__ __forceinline__ void chol16_pivot(Blk16& b, int r, int g, int& fail) {
   constexpr int GJ = J >> 2, QJ = J & 3;
   const double piv = readlane_f64(b.a[QJ], J + 16 * GJ);
-  const double arj = bpermute_f64(r + 16 * GJ, b.a[QJ]);  // A[r][J]
+  const double arj = xrow_bcast_f64<GJ>(b.a[QJ]);  // A[r][J]
   double aj[4], xj[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {

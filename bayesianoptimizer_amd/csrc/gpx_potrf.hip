@@ -20,7 +20,9 @@
 //    update is traffic-bound at 64x64: 36 us for the 2016 tiles of step 0).
 // Column c+1 is thus updated by step c-1 in launch c and by step c inside the panel workgroups of launch c+1, so
 // the panel factorisation (the latency-bound serial chain) overlaps the trailing update of the previous step
-// instead of following it.  potrf_dinv finally copies every L_kk from the scratch into A and inverts it (Dinv, used
+// instead of following it.  For large n the trailing update is flushed lazily (every g block columns, K = 64 g:
+// each C tile read and written once per g columns) and lookahead workgroups bring the next panel's column up to
+// date in the launch before it (StepPlan below).  potrf_dinv finally copies every L_kk from the scratch into A and inverts it (Dinv, used
 // by gpx_trtri_f64).
 #include "gpx_internal.h"
 #include "gpx_device.h"
@@ -75,7 +77,7 @@ __device__ __forceinline__ void load_tile_lds(const double* __restrict__ G, int6
 }
 
 // Panel workgroup p of block column c (see the file comment).
-__device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, int c, int p, int nblk, int lazy,
+__device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, int c, int p, int nblk, int c0,
                                            double* __restrict__ Dinv, int32_t* __restrict__ info, double* lds) {
   double* sA = lds;             // A_cc -> L_cc
   double* sP = sA + NB * LD64;  // A_ic -> L_ic (p > 0)
@@ -90,9 +92,8 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
   double* Aic = A + (int64_t)bi * NB * lda + (int64_t)c * NB;
   if (t == 0) s_tdone = 0;
   if (c > 0) {
-    // the updates of block columns c0 .. c-1 not yet applied by a trailing flush, on the two tiles this workgroup
-    // factors (K = 64 (c - c0) <= 64 lazy)
-    const int c0 = lazy * ((c - 1) / lazy);
+    // the updates of block columns c0 .. c-1 not yet applied to this column, on the two tiles this workgroup
+    // factors (K = 64 (c - c0))
     const int kk = (c - c0) * NB;
     const double* Lc = A + (int64_t)c * NB * lda + (int64_t)c0 * NB;
     Tile64 tl;
@@ -191,12 +192,12 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
 }
 
 // Trailing workgroup of a flush launch c (c % lazy == 0): 128x128 tile `tile` of the lower triangle of block columns
-// >= c+1, A_ij -= sum_{k = c-lazy}^{c-1} L_ik L_jk^T (K = 64 lazy).  The 128-grid is aligned to the end of the matrix
+// >= cfirst, A_ij -= sum_{k = c-lazy}^{c-1} L_ik L_jk^T (K = 64 lazy).  The 128-grid is aligned to the end of the matrix
 // (first 64-block c0 = nblk - 2M); when it starts at block c, that block row/column is computed but not stored (it
 // belongs to this launch's panel).
-__device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t lda, int c, int nblk, int lazy, int tile,
-                                              double* lds) {
-  const int m = nblk - c - 1;
+__device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t lda, int c, int nblk, int lazy, int cfirst,
+                                              int tile, double* lds) {
+  const int m = nblk - cfirst;
   const int M = (m + 1) / 2;
   const int c0 = nblk - 2 * M;
   int I, J;
@@ -221,25 +222,78 @@ __device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t ld
       for (int r = 0; r < 4; ++r) {
         const int row = Tile128::row_of(i, r), col = Tile128::col_of(j);
         const int rb = r0 + (row >> 6), cb = q0 + (col >> 6);
-        if (cb > c && rb >= cb) C[(int64_t)row * lda + col] = cv[j][r] - tl.acc[i][j][r];
+        if (cb >= cfirst && rb >= cb) C[(int64_t)row * lda + col] = cv[j][r] - tl.acc[i][j][r];
       }
   }
 }
 
+// Lookahead workgroup (mode 1) of launch c: tile (c+1+idx, c+1) of the next panel's column gets every pending
+// update, A_i,c+1 -= sum_{k = a}^{c-1} L_ik L_{c+1,k}^T with a = the first column no flush has applied to it, so
+// that the panels always apply exactly one column (K = 64 on the critical path) while the bulk of the trailing
+// matrix is flushed every `lazy` launches.
+__device__ __forceinline__ void lookahead_role(double* __restrict__ A, int64_t lda, int c, int a, int idx, double* lds) {
+  const int i = c + 1 + idx, j = c + 1;
+  const double* Li = A + (int64_t)i * NB * lda + (int64_t)a * NB;
+  const double* Lj = A + (int64_t)j * NB * lda + (int64_t)a * NB;
+  double* C = A + (int64_t)i * NB * lda + (int64_t)j * NB;
+  Tile64 tl;
+  tl.run(Li, lda, Lj, lda, 0, (c - a) * NB, lds);
+#pragma unroll
+  for (int ii = 0; ii < Tile64::WM; ++ii)
+#pragma unroll
+    for (int jj = 0; jj < Tile64::WN; ++jj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double* Cp = C + (int64_t)Tile64::row_of(ii, r) * lda + Tile64::col_of(jj);
+        *Cp = *Cp - tl.acc[ii][jj][r];
+      }
+}
+
+// Work split of launch c.  mode 0: the panels apply the pending columns c0 .. c-1 (c0 = the last flush), the flush
+// (c % lazy == 0) covers columns >= c+1.  mode 1: the panels apply column c-1 only, lookahead workgroups bring
+// column c+1 up to date, the flush covers columns >= c+2.
+struct StepPlan {
+  int npanel, nlook, ntrail, c0, look_a, cfirst;
+  bool flush;
+};
+
+__host__ __device__ inline StepPlan step_plan(int c, int nblk, int lazy, int mode) {
+  StepPlan s;
+  s.npanel = nblk - c;
+  s.flush = c >= lazy && c % lazy == 0;
+  if (mode == 0) {
+    s.c0 = c > 0 ? lazy * ((c - 1) / lazy) : 0;
+    s.nlook = 0;
+    s.look_a = 0;
+    s.cfirst = c + 1;
+  } else {
+    s.c0 = c > 0 ? c - 1 : 0;
+    s.nlook = (c >= 1 && c + 1 < nblk) ? nblk - c - 1 : 0;
+    s.look_a = c > 0 ? lazy * ((c - 1) / lazy) : 0;
+    s.cfirst = c + 2;
+  }
+  const int m = nblk - s.cfirst;
+  const int M = (s.flush && m > 0) ? (m + 1) / 2 : 0;
+  s.ntrail = M * (M + 1) / 2;
+  return s;
+}
+
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
-potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, int lazy, double* __restrict__ Dinv,
+potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, int lazy, int mode, double* __restrict__ Dinv,
                   int32_t* __restrict__ info, int first_wg, int64_t sa, int64_t sd) {
   A += blockIdx.y * sa;  // problem of a batched fit
   Dinv += blockIdx.y * sd;
   info += blockIdx.y;
   if (*(volatile int32_t*)info != 0) return;  // an earlier step failed: leave the rest untouched
   __shared__ __attribute__((aligned(16))) double lds[STEP_LDS];
-  const int npanel = nblk - c;
+  const StepPlan s = step_plan(c, nblk, lazy, mode);
   const int b = first_wg + (int)blockIdx.x;
-  if (b < npanel)
-    panel_role(A, lda, c, b, nblk, lazy, Dinv, info, lds);
+  if (b < s.npanel)
+    panel_role(A, lda, c, b, nblk, s.c0, Dinv, info, lds);
+  else if (b < s.npanel + s.nlook)
+    lookahead_role(A, lda, c, s.look_a, b - s.npanel, lds);
   else
-    trailing_role(A, lda, c, nblk, lazy, b - npanel, lds);
+    trailing_role(A, lda, c, nblk, lazy, s.cfirst, b - s.npanel - s.nlook, lds);
 }
 
 // L_kk from the scratch into A, and D_k = L_kk^{-1} into the first half of Dinv (one workgroup per block).
@@ -277,28 +331,40 @@ __global__ void __launch_bounds__(WG) potrf_dinv_kernel(double* __restrict__ A, 
 // K = 128 panel pre-update sits on the critical path, the trailing update mostly hides under the panel chain);
 // n = 8192: lazy 1/2/4 -> 7.05/6.75/7.21 ms; n = 16384: lazy 1/2/4/8 -> 46.3/37.4/34.3/35.3 ms (the trailing update
 // dominates).  GPX_POTRF_LAZY overrides.
-static int potrf_lazy(int nblk) {
-  static const int env = [] {
-    const char* e = std::getenv("GPX_POTRF_LAZY");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (env > 0) return env > 8 ? 8 : env;
-  return nblk > 128 ? 4 : (nblk > 64 ? 2 : 1);
+// Schedule by size (tools/lazy_sweep.sh, profiles/r01_potrf_lazy_sweep*.log):
+//   n = 4096:  mode 0, g = 1 -> potrf 1.73-1.75 ms (mode 1 g = 2/4: 1.81/1.94: a K = 128 flush tile is >= 14 us of
+//              MFMA on one CU, longer than the ~20 us panel window once two share a CU);
+//   n = 8192:  mode 1, g = 4 -> 6.34 ms (mode 0 g = 2: 6.69);
+//   n = 16384: mode 1, g = 8 -> 31.4 ms (mode 0 g = 4: 34.4, g = 1: 46.3).
+// GPX_POTRF_MODE / GPX_POTRF_LAZY override.
+static int env_int(const char* name) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : -1;
 }
 
-int potrf_step_grid(int c, int nblk, int lazy) {
-  const int m = nblk - c - 1;
-  const bool flush = c >= lazy && c % lazy == 0;
-  const int M = (flush && m > 0) ? (m + 1) / 2 : 0;
-  return (nblk - c) + M * (M + 1) / 2;
+static int potrf_lazy(int nblk) {
+  static const int env = env_int("GPX_POTRF_LAZY");
+  if (env > 0) return env > 16 ? 16 : env;
+  return nblk > 128 ? 8 : (nblk > 64 ? 4 : 1);
+}
+
+static int potrf_mode(int nblk) {
+  static const int env = env_int("GPX_POTRF_MODE");
+  if (env == 0 || env == 1) return env;
+  return nblk > 64 ? 1 : 0;
+}
+
+int potrf_step_grid(int c, int nblk, int lazy, int mode) {
+  const StepPlan s = step_plan(c, nblk, lazy, mode);
+  return s.npanel + s.nlook + s.ntrail;
 }
 
 static void launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
                          int cbeg, int cend) {
-  const int lazy = potrf_lazy(nblk);
+  const int lazy = potrf_lazy(nblk), mode = potrf_mode(nblk);
   for (int c = cbeg; c < cend; ++c)
-    potrf_step_kernel<<<dim3(potrf_step_grid(c, nblk, lazy), bt.count), WG, 0, ctx->stream>>>(
-        A, lda, c, nblk, lazy, Dinv, info, 0, bt.k, bt.dinv);
+    potrf_step_kernel<<<dim3(potrf_step_grid(c, nblk, lazy, mode), bt.count), WG, 0, ctx->stream>>>(
+        A, lda, c, nblk, lazy, mode, Dinv, info, 0, bt.k, bt.dinv);
 }
 
 static void launch_dinv(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,

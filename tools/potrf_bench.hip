@@ -130,26 +130,26 @@ int main(int argc, char** argv) {
   // per-launch times of step c (after running steps 0..c-1 once): full grid, panel workgroups only
   auto time_step = [&](int c, int mode) {  // 0 full grid, 1 panel workgroups only, 2 trailing workgroups only
     CK(hipMemcpy(A, A0, (size_t)n * n * 8, hipMemcpyDeviceToDevice)); CK(hipMemset(info, 0, 4));
-    for (int cc = 0; cc < c; ++cc) potrf_step_kernel<<<potrf_step_grid(cc, nblk, 1), WG>>>(A, n, cc, nblk, 1, Dinv, info, 0, 0, 0);
+    for (int cc = 0; cc < c; ++cc) potrf_step_kernel<<<potrf_step_grid(cc, nblk, 1, 0), WG>>>(A, n, cc, nblk, 1, 0, Dinv, info, 0, 0, 0);
     CK(hipDeviceSynchronize());
-    const int full = potrf_step_grid(c, nblk, 1);
+    const int full = potrf_step_grid(c, nblk, 1, 0);
     const int grid = mode == 0 ? full : mode == 1 ? nblk - c : full - (nblk - c);
     const int first = mode == 2 ? nblk - c : 0;
     CK(hipEventRecord(e0));
-    for (int i = 0; i < 20; ++i) potrf_step_kernel<<<grid, WG>>>(A, n, c, nblk, Dinv, info, first);
+    for (int i = 0; i < 20; ++i) potrf_step_kernel<<<grid, WG>>>(A, n, c, nblk, 1, 0, Dinv, info, first, 0, 0);
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     int hi; CK(hipMemcpy(&hi, info, 4, hipMemcpyDeviceToHost));
     return hi ? -1.0f : ms * 50.0f;
   };
-  const float td = timeit([&] { for (int i = 0; i < 20; ++i) potrf_dinv_kernel<<<nblk, WG>>>(A, n, nblk, Dinv, info); }, 5);
+  const float td = timeit([&] { for (int i = 0; i < 20; ++i) potrf_dinv_kernel<<<nblk, WG>>>(A, n, nblk, Dinv, info, 0, 0, 0); }, 5);
   for (int c : {1, 8, 16, 32, 48, nblk - 3})
     printf("step %2d: %6.2f us   panel wgs only %6.2f us   trailing wgs only %6.2f us (%d tiles)\n", c, time_step(c, 0),
-           time_step(c, 1), time_step(c, 2), potrf_step_grid(c, nblk, 1) - (nblk - c));
+           time_step(c, 1), time_step(c, 2), potrf_step_grid(c, nblk, 1, 0) - (nblk - c));
   printf("dinv: %.2f us\n", td * 50);
   CK(hipMemcpy(A, A0, (size_t)n * n * 8, hipMemcpyDeviceToDevice)); CK(hipMemset(info, 0, 4));
-  potrf_step_kernel<<<potrf_step_grid(0, nblk, 1), WG>>>(A, n, 0, nblk, 1, Dinv, info, 0, 0, 0); CK(hipDeviceSynchronize());
-  potrf_step_kernel<<<potrf_step_grid(1, nblk, 1), WG>>>(A, n, 1, nblk, 1, Dinv, info, 0, 0, 0); CK(hipDeviceSynchronize());
+  potrf_step_kernel<<<potrf_step_grid(0, nblk, 1, 0), WG>>>(A, n, 0, nblk, 1, 0, Dinv, info, 0, 0, 0); CK(hipDeviceSynchronize());
+  potrf_step_kernel<<<potrf_step_grid(1, nblk, 1, 0), WG>>>(A, n, 1, nblk, 1, 0, Dinv, info, 0, 0, 0); CK(hipDeviceSynchronize());
   unsigned long long hs[4][16]; CK(hipMemcpyFromSymbol(hs, HIP_SYMBOL(g_stamp), sizeof(hs)));
   unsigned hw[4]; CK(hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_hwid), sizeof(hw)));
   for (int w = 0; w < 4; ++w) printf("wave %d HW_ID 0x%08x (simd %u, cu %u)\n", w, hw[w], (hw[w] >> 4) & 3, (hw[w] >> 8) & 15);
