@@ -48,6 +48,8 @@ def parse():
                     help="independent problems (restarts/seeds) per GPU per step; 4 at 8 GPUs = BASELINE configs[3]")
     ap.add_argument("--cpu-sample", type=int, default=8192, help="candidates in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="skip the side measurements of BASELINE configs[2] and configs[4] (N=1 only)")
     return ap.parse_args()
 
 
@@ -158,6 +160,50 @@ def cpu_baseline(X, y, Xs_np, kind, acq, ls, sample, reps=3):
                       f"faster of: " + "; ".join(f"{c['what'].split(':')[0]} {c['value']:.4g}" for c in cands)}
 
 
+def other_configs(eng, dev, seed):
+    """Side measurements at N=1 of the other GPU configs of BASELINE.json (not the headline `value`):
+    configs[2] n=16384 d=8 Matern-5/2 posterior update, configs[4] n=4096 d=16 fp32 covariance build + UCB sweep."""
+    out = {}
+    X_np, y_np = synthetic.problem(16384, 8, seed + 7)
+    X, y = torch.tensor(X_np, device=dev), torch.tensor(y_np, device=dev)
+    p = KernelParams("matern52", botorch_default_lengthscale(8), noise=1e-4)
+    st = eng.fit(X, y, p)
+    ts = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        st = eng.fit(X, y, p, check=False, out=st)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - a)
+    if st.pivot_failure() >= 0:
+        raise RuntimeError("configs[2] Cholesky failed")
+    t = float(np.median(ts))
+    out["configs[2]"] = {"workload": "n=16384 d=8 Matern-5/2 fp64 posterior update (Gram + Cholesky + L^-T + alpha)",
+                         "fit_ms": 1e3 * t, "updates_per_s": 1.0 / t,
+                         "cholesky_plus_inverse_tflops": 2 * 16384.0 ** 3 / 3 / t / 1e12}
+    del st, X, y
+    torch.cuda.empty_cache()
+    X_np, y_np = synthetic.problem(4096, 16, seed + 11)
+    Xs_np = synthetic.sobol(1 << 20, 16, seed + 12)
+    X, y, Xs = (torch.tensor(v, device=dev) for v in (X_np, y_np, Xs_np))
+    p = KernelParams("rbf", botorch_default_lengthscale(16), noise=1e-4, cov_fp32=True)
+    st = eng.fit(X, y, p)
+    eng.acquire(st, Xs, "ucb", beta=4.0)
+    ts = []
+    for _ in range(2):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        st = eng.fit(X, y, p, check=False, out=st)
+        bv, bi = eng.acquire(st, Xs, "ucb", beta=4.0)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - a)
+    t = float(np.median(ts))
+    out["configs[4]"] = {"workload": "n=4096 d=16 RBF, fp32 covariance build, fp64 factorisation, 1048576-candidate "
+                                     "UCB sweep + argmax", "ms_per_step": 1e3 * t, "acq_cands_per_s": (1 << 20) / t,
+                         "best_index": int(bi.item())}
+    return out
+
+
 def main():
     args = parse()
     dist, rank, world, local = dist_setup(args)
@@ -244,6 +290,9 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(X_np, y_np, Xs_np, args.kernel, args.acq, ls, args.cpu_sample)
+        extra = None
+        if world == 1 and not args.no_other_configs:
+            extra = other_configs(eng, dev, args.seed)
         out = {
             "metric": METRIC,
             "value": value,
@@ -282,6 +331,7 @@ def main():
                 "flops_per_launch": flops_per_launch,
             },
             "cpu_baseline": cpu,
+            "other_configs": extra,
         }
         print(json.dumps(out))
     if dist is not None:
