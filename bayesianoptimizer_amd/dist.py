@@ -98,3 +98,20 @@ def sharded_best(num_units: int, local_best: Callable[[int], Tuple[torch.Tensor,
         bi = torch.tensor([2 ** 63 - 1], dtype=torch.int64, device=dev)
     v, i = exchange_argmax(bv, bi, engine=engine, group=group)
     return v, i, results
+
+
+def sharded_sweep(engine, state, Xs: torch.Tensor, kind: str = "logei", group=None, **acq_kwargs):
+    """One fit, many candidates: every rank holds the same fitted ``state`` (the factorisation
+    is recomputed on each GPU — ~2.5 ms at n = 4096, cheaper than broadcasting 128 MiB of L) and scores its
+    contiguous shard [start, stop) of the global candidate set ``Xs`` (m x d, identical on every rank); the
+    (value, global index) records are then exchanged once.  Returns (value, index) 1-element tensors."""
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    start, stop = shard_range(Xs.shape[0], rank, world)
+    if stop > start:
+        bv, bi = engine.acquire(state, Xs[start:stop], kind, index_offset=start, **acq_kwargs)
+    else:
+        dev = Xs.device
+        bv = torch.tensor([float("-inf")], dtype=torch.float64, device=dev)
+        bi = torch.tensor([2 ** 63 - 1], dtype=torch.int64, device=dev)
+    return exchange_argmax(bv, bi, engine=engine, group=group)

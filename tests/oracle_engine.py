@@ -85,7 +85,7 @@ class OracleEngine:
         mu, var = O.posterior(st1, Xs, y_mean, y_scale)
         scores = O.acquisition(mu, var, ACQS[kind] if isinstance(kind, str) else int(kind), best_f, beta)
         v, i = O.argmax_lowest(scores)
-        out = (torch.tensor([v]), torch.tensor([i + index_offset]))
+        out = (torch.tensor([v], dtype=torch.float64), torch.tensor([i + index_offset], dtype=torch.int64))
         return out + (torch.tensor(scores),) if return_scores else out
 
     def moments_grad(self, state, Xs, q=1, alpha=None):

@@ -75,3 +75,48 @@ def test_sharded_best_world2(num_units):
     assert out[0][1] == pytest.approx(best[0], rel=0, abs=0) and out[0][2] == best[1]
     # tie -> lowest index (rank 1 offered index 9)
     assert out[0][4:] == (1.0, 9) and out[1][4:] == (1.0, 9)
+
+
+def _sweep_worker(rank, world, port, m, q):
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from bayesianoptimizer_amd.dist import sharded_sweep
+        from bayesianoptimizer_amd.engine import KernelParams
+        from oracle import gp_oracle as O
+        from tests.oracle_engine import OracleEngine
+
+        X, y = O.synthetic_problem(80, 3, 4)
+        Xs = torch.tensor(O.sobol_candidates(m, 3, 5))
+        eng = OracleEngine()
+        st = eng.fit(torch.tensor(X), torch.tensor(y), KernelParams("rbf", 0.4, noise=1e-4))
+        v, i = sharded_sweep(eng, st, Xs, "logei", best_f=float(y.max()))
+        q.put((rank, float(v), int(i)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,m", [(2, 1000), (3, 2)])
+def test_sharded_sweep_one_fit_many_candidates(world, m):
+    # the same fit on every rank, contiguous candidate shards, one record exchange
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sweep_worker, args=(r, world, port, m, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from oracle import gp_oracle as O
+
+    X, y = O.synthetic_problem(80, 3, 4)
+    st = O.fit(X, y, O.KernelParams(O.RBF, np.full(3, 0.4), noise=1e-4))
+    v_ref, i_ref, _ = O.acquire_argmax(st, O.sobol_candidates(m, 3, 5), O.ACQ_LOGEI, best_f=float(y.max()))
+    for _, v, i in out:
+        assert i == i_ref and v == pytest.approx(v_ref, rel=1e-12)
