@@ -119,4 +119,4 @@ def test_sharded_sweep_one_fit_many_candidates(world, m):
     st = O.fit(X, y, O.KernelParams(O.RBF, np.full(3, 0.4), noise=1e-4))
     v_ref, i_ref, _ = O.acquire_argmax(st, O.sobol_candidates(m, 3, 5), O.ACQ_LOGEI, best_f=float(y.max()))
     for _, v, i in out:
-        assert i == i_ref and v == pytest.approx(v_ref, rel=1e-12)
+        assert i == i_ref and v == pytest.approx(v_ref, rel=1e-10)  # shard vs full-set BLAS blocking
