@@ -422,7 +422,7 @@ def test_fit_batched_reports_not_pd_per_problem(engine):
         engine.fit_batched(t(Xs), t(np.zeros((B, n))), kp)
 
 
-@pytest.mark.parametrize("n,kind", [(8192, "rbf"), (16384, "matern52")])
+@pytest.mark.parametrize("n,kind", [(8192, "rbf"), (16384, "matern52"), (32768, "rbf")])
 def test_large_fit_inverse_and_factor_rows(engine, n, kind):
     # sizes whose TRTRI uses the 128x128-tile levels and whose Cholesky uses the lazy trailing flush
     d = 8

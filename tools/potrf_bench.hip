@@ -150,13 +150,19 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(A, A0, (size_t)n * n * 8, hipMemcpyDeviceToDevice)); CK(hipMemset(info, 0, 4));
   potrf_step_kernel<<<potrf_step_grid(0, nblk, 1, 0), WG>>>(A, n, 0, nblk, 1, 0, Dinv, info, 0, 0, 0); CK(hipDeviceSynchronize());
   potrf_step_kernel<<<potrf_step_grid(1, nblk, 1, 0), WG>>>(A, n, 1, nblk, 1, 0, Dinv, info, 0, 0, 0); CK(hipDeviceSynchronize());
-  unsigned long long hs[4][16]; CK(hipMemcpyFromSymbol(hs, HIP_SYMBOL(g_stamp), sizeof(hs)));
-  unsigned hw[4]; CK(hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_hwid), sizeof(hw)));
-  for (int w = 0; w < 4; ++w) printf("wave %d HW_ID 0x%08x (simd %u, cu %u)\n", w, hw[w], (hw[w] >> 4) & 3, (hw[w] >> 8) & 15);
-  for (int w = 0; w < 4; ++w) {
-    printf("wave %d stamps (cycles after load):", w);
-    for (int i = 1; i <= 13; ++i) printf(" %lld", (long long)(hs[w][i] - hs[0][0]));
-    printf("\n");
+  for (int rep = 0; rep < 3; ++rep) {
+    if (rep > 0) {  // the same step again (warm instruction cache on the CUs that ran it)
+      potrf_step_kernel<<<potrf_step_grid(1, nblk, 1, 0), WG>>>(A, n, 1, nblk, 1, 0, Dinv, info, 0, 0, 0);
+      CK(hipDeviceSynchronize());
+    }
+    unsigned long long hs[4][16]; CK(hipMemcpyFromSymbol(hs, HIP_SYMBOL(g_stamp), sizeof(hs)));
+    unsigned hw[4]; CK(hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_hwid), sizeof(hw)));
+    printf("rep %d: wave 0 on cu %u\n", rep, (hw[0] >> 8) & 15);
+    for (int w = 0; w < 1; ++w) {
+      printf("wave %d stamps (cycles after load):", w);
+      for (int i = 1; i <= 13; ++i) printf(" %lld", (long long)(hs[w][i] - hs[0][0]));
+      printf("\n");
+    }
   }
   printf("POTRF BENCH DONE\n");
   return 0;
