@@ -20,6 +20,7 @@ GPX_MAX_RHS = 8
 GPX_TILE = 128
 GPX_MAX_Q = 32
 GPX_MAX_GRAD_CANDIDATES = 16384
+GPX_COMM_ID_BYTES = 128
 
 GPX_OK, GPX_NOT_PD, GPX_INVALID_ARG, GPX_HIP_ERROR, GPX_RCCL_ERROR = 0, 1, 2, 3, 4
 STATUS_NAMES = {0: "OK", 1: "NOT_PD", 2: "INVALID_ARG", 3: "HIP_ERROR", 4: "RCCL_ERROR"}
@@ -116,6 +117,11 @@ _PROTOS = {
                                          c_int64, c_int64, POINTER(AcqParamsC), c_int64, _p, _p, _p, _p,
                                          c_size_t]),
     "gpx_argmax_combine_f64": (c_int32, [_h, _p, _p, c_int64, _p, _p]),
+    "gpx_comm_unique_id": (c_int32, [c_void_p]),
+    "gpx_comm_init": (c_int32, [_h, c_void_p, c_int32, c_int32, POINTER(c_void_p)]),
+    "gpx_comm_destroy": (c_int32, [c_void_p]),
+    "gpx_allreduce_argmax_workspace_size": (c_int32, [c_void_p, POINTER(c_size_t)]),
+    "gpx_allreduce_argmax": (c_int32, [_h, c_void_p, _p, _p, _p, c_size_t]),
     "gpx_mll_workspace_size": (c_int32, [c_int64, POINTER(c_size_t)]),
     "gpx_mll_grad_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, c_int64, _p,
                                    c_int64, _p, c_int64, _p, _p, _p, c_size_t]),

@@ -9,6 +9,7 @@ RCCL has no MAXLOC op, hence gather + local reduce instead of an all-reduce.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
@@ -115,3 +116,58 @@ def sharded_sweep(engine, state, Xs: torch.Tensor, kind: str = "logei", group=No
         bv = torch.tensor([float("-inf")], dtype=torch.float64, device=dev)
         bi = torch.tensor([2 ** 63 - 1], dtype=torch.int64, device=dev)
     return exchange_argmax(bv, bi, engine=engine, group=group)
+
+
+class RCCLArgmaxExchange:
+    """The record exchange through libgpx's own RCCL communicator (gpx_allreduce_argmax, include/gpx.h): rank 0 makes
+    the communicator id, torch.distributed broadcasts its 128 bytes once, then every exchange is one RCCL all-gather
+    of the 16-byte records plus the argmax_combine kernel on the engine's stream — no torch collective on the hot
+    path.  ``__call__(val, idx)`` replaces the device records in place by the global best and returns them."""
+
+    def __init__(self, engine, group=None):
+        from . import _capi
+
+        self.engine = engine
+        self.lib = engine.lib
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        buf = (ctypes.c_ubyte * _capi.GPX_COMM_ID_BYTES)()
+        if rank == 0:
+            _capi.check(self.lib.gpx_comm_unique_id(ctypes.cast(buf, ctypes.c_void_p)))
+        if world > 1:
+            backend = dist.get_backend(group)
+            dev = engine.device if backend == "nccl" else torch.device("cpu")
+            t = torch.tensor(list(buf), dtype=torch.uint8, device=dev)
+            dist.broadcast(t, src=0, group=group)
+            for k, v in enumerate(t.cpu().tolist()):
+                buf[k] = v
+        self.comm = ctypes.c_void_p()
+        _capi.check(self.lib.gpx_comm_init(engine.handle, ctypes.cast(buf, ctypes.c_void_p), world, rank,
+                                           ctypes.byref(self.comm)), engine.handle)
+        nbytes = ctypes.c_size_t()
+        _capi.check(self.lib.gpx_allreduce_argmax_workspace_size(self.comm, ctypes.byref(nbytes)))
+        self.ws = torch.empty(nbytes.value, dtype=torch.uint8, device=engine.device)
+
+    def __call__(self, val: torch.Tensor, idx: torch.Tensor):
+        from . import _capi
+
+        if val.dtype != torch.float64 or idx.dtype != torch.int64 or not val.is_cuda or val.numel() != 1 \
+                or idx.numel() != 1:
+            raise ValueError("records must be 1-element fp64 / int64 device tensors")
+        self.engine._bind_stream()
+        _capi.check(self.lib.gpx_allreduce_argmax(self.engine.handle, self.comm, ctypes.c_void_p(val.data_ptr()),
+                                                  ctypes.c_void_p(idx.data_ptr()),
+                                                  ctypes.c_void_p(self.ws.data_ptr()), self.ws.numel()),
+                    self.engine.handle)
+        return val, idx
+
+    def close(self):
+        if self.comm:
+            self.lib.gpx_comm_destroy(self.comm)
+            self.comm = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -37,6 +37,8 @@ extern "C" {
 #define GPX_MAX_GRAD_CANDIDATES 16384  /* candidates per gpx_moments_grad_f64 call */
 
 typedef struct gpx_context* gpx_handle;
+typedef struct gpx_comm_s* gpx_comm;   /* RCCL communicator of the cross-GPU record exchange */
+#define GPX_COMM_ID_BYTES 128          /* ncclUniqueId */
 typedef int32_t gpx_status;
 
 enum {
@@ -228,6 +230,20 @@ gpx_status gpx_moments_grad_f64(gpx_handle h, const gpx_kernel_params* p, int64_
                                 const double* W, int64_t ldw, const double* alpha, const double* Xs, int64_t m,
                                 int64_t q, int64_t ldxs, double* mean, double* dmean, double* cov, double* dcov,
                                 void* ws, size_t ws_bytes);
+
+/* ---- cross-GPU selection exchange (SURVEY §8b gpx_allreduce_argmax, §8e) ------------------------------------------ */
+/* One process per GPU.  Rank 0 creates the communicator id (gpx_comm_unique_id), the host side broadcasts its
+ * GPX_COMM_ID_BYTES bytes (e.g. over torch.distributed), every rank calls gpx_comm_init (collective).
+ * gpx_allreduce_argmax replaces every rank's device (best_val, best_idx) record by the global best: an RCCL
+ * all-gather of the 16-byte records over xGMI, then the argmax_combine kernel (max value, lowest global index, NaN
+ * never wins) on the handle's stream — RCCL has no MAXLOC.  Replaces the final best-candidate selection across the
+ * independent restarts/shards (BASELINE configs[3]). */
+gpx_status gpx_comm_unique_id(uint8_t* id_out);
+gpx_status gpx_comm_init(gpx_handle h, const uint8_t* id, int32_t nranks, int32_t rank, gpx_comm* out);
+gpx_status gpx_comm_destroy(gpx_comm c);
+gpx_status gpx_allreduce_argmax_workspace_size(gpx_comm c, size_t* bytes);
+gpx_status gpx_allreduce_argmax(gpx_handle h, gpx_comm c, double* best_val, int64_t* best_idx, void* ws,
+                                size_t ws_bytes);
 
 /* ---- marginal likelihood -------------------------------------------------------- */
 /* Negative log marginal likelihood of a fitted exact GP with T = nrhs outputs sharing the covariance (T = 1:

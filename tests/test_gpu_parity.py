@@ -444,3 +444,19 @@ def test_large_fit_inverse_and_factor_rows(engine, n, kind):
     ost_rows = O.sobol_candidates(64, d, 3)
     mu, var = engine.posterior(st, t(ost_rows))
     assert torch.isfinite(mu).all() and bool((var > 0).all())
+
+
+def test_rccl_record_exchange_single_rank(engine):
+    # gpx_allreduce_argmax on a one-rank libgpx RCCL communicator: the record comes back unchanged; the
+    # multi-rank host logic is covered by the gloo tests (tests/test_dist_gloo.py)
+    from bayesianoptimizer_amd.dist import RCCLArgmaxExchange
+
+    ex = RCCLArgmaxExchange(engine)
+    v = torch.tensor([3.5], dtype=torch.float64, device=DEV)
+    i = torch.tensor([42], dtype=torch.int64, device=DEV)
+    ex(v, i)
+    assert float(v.item()) == 3.5 and int(i.item()) == 42
+    v.fill_(float("nan"))
+    ex(v, i)
+    assert float(v.item()) == float("-inf") and int(i.item()) == 42  # NaN never wins
+    ex.close()
