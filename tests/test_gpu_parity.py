@@ -460,3 +460,14 @@ def test_rccl_record_exchange_single_rank(engine):
     ex(v, i)
     assert float(v.item()) == float("-inf") and int(i.item()) == 42  # NaN never wins
     ex.close()
+
+
+def test_c_abi_example_program():
+    # the boundary used from plain C (tools/capi_example.c, built by __graft_entry__.build()): fit + sweep through
+    # include/gpx.h with hipMalloc'd buffers, alpha checked against a host Cholesky
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "capi_example")
+    assert os.path.exists(exe), "build the C example with __graft_entry__.build()"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "capi example ok" in r.stdout, r.stdout + r.stderr
