@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <algorithm>
 #include "../bayesianoptimizer_amd/csrc/gpx_mll.hip"
 
 namespace gpx {  // launch_mll is not used here; satisfy its timer references
@@ -79,29 +80,29 @@ int main() {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const double flops = (double)npad * npad * npad / 3.0;
-  const char* names[] = {"p0 product row-major kc=512", "p0 product row-major kc=npad",
-                         "p1 product k-major   kc=512", "p1 product k-major   kc=npad",
-                         "p2 mll_grad_kernel<8> kc=512", "p2 mll_grad_kernel<8> kc=npad"};
-  auto launch = [&](int v) {
-    const int kc = (v % 2 == 0) ? 512 : npad;
+  // kc sweep of the full kernel (product + epilogue) and of the product alone
+  const int kcs[] = {384, 512, 768, 1024, 1536, 2048, 4096};
+  for (int kc : kcs) {
+    if (kc > npad) continue;
     const dim3 grid(tiles, (npad + kc - 1) / kc);
-    if (v < 2) product_only<false><<<grid, WG>>>(W, npad, npad, kc, sink);
-    else if (v < 4) product_only<true><<<grid, WG>>>(Wt, npad, npad, kc, sink);
-    else mll_grad_kernel<8><<<grid, WG>>>(p, n, npad, X, d, W, npad, al, kc, part);
-  };
-  double tot[6] = {0};
-  for (int rep = 0; rep < 6; ++rep)
-    for (int v = 0; v < 6; ++v) {
-      launch(v);
-      CK(hipEventRecord(e0));
-      for (int r = 0; r < 5; ++r) launch(v);
-      CK(hipEventRecord(e1));
-      CK(hipEventSynchronize(e1));
-      float ms;
-      CK(hipEventElapsedTime(&ms, e0, e1));
-      if (rep > 0) tot[v] += ms / 5;
-    }
-  for (int v = 0; v < 6; ++v)
-    printf("%-32s %8.3f ms  %6.1f TF/s (n^3/3)\n", names[v], tot[v] / 5, flops / (tot[v] / 5 * 1e-3) / 1e12);
+    float best[2] = {1e30f, 1e30f};
+    for (int rep = 0; rep < 6; ++rep)
+      for (int v = 0; v < 2; ++v) {
+        auto go = [&] {
+          if (v == 0) product_only<false><<<grid, WG>>>(W, npad, npad, kc, sink);
+          else mll_grad_kernel<8><<<grid, WG>>>(p, n, npad, X, d, W, npad, al, 1, kc, part);
+        };
+        go();
+        CK(hipEventRecord(e0));
+        for (int r = 0; r < 5; ++r) go();
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        best[v] = std::min(best[v], ms / 5);
+      }
+    printf("kc=%5d units=%6d  product %.3f ms (%.1f TF/s)  full %.3f ms (%.1f TF/s)\n", kc, tiles * (int)grid.y,
+           best[0], flops / (best[0] * 1e-3) / 1e12, best[1], flops / (best[1] * 1e-3) / 1e12);
+  }
   return 0;
 }
