@@ -4,7 +4,7 @@
 // Register layout of a 16x16 block in a wave: lane = r + 16 g owns row r, columns 4g..4g+3.  At pivot j the pivot
 // A[j][j] is one lane's register (v_readlane, uniform); every lane applies the unscaled rank-1 update
 // A[r][c] -= A[r][j] A[j][c] / A[j][j] and the same row operation on X = L^{-1}, with the cross-lane operands moved
-// by DPP and ds_bpermute, so only the pivot's rsq sits between two consecutive pivots.  LDS tiles use a padded row
+// by DPP and gfx950 permlane swaps, so only the pivot's rsq sits between two consecutive pivots.  LDS tiles use a padded row
 // length LD64 (doubles).
 #pragma once
 #include <utility>
@@ -49,14 +49,6 @@ __device__ __forceinline__ double row_bcast(double v) {
   const unsigned long long u = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_mov_dpp((int)(u & 0xffffffffull), 0x150 + J, 0xf, 0xf, false);
   const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), 0x150 + J, 0xf, 0xf, false);
-  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
-}
-
-// Value of lane `src_lane` (any lane of the wave), as a double: two ds_bpermute_b32 (LDS crossbar, no bank access).
-__device__ __forceinline__ double bpermute_f64(int src_lane, double v) {
-  const unsigned long long u = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(u & 0xffffffffull));
-  const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(u >> 32));
   return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 

@@ -317,6 +317,13 @@ def main():
             },
             "updates_per_s": world * P * fit_reps / fit_elapsed,
             "fit_ms": 1e3 * fit_elapsed / fit_reps,
+            # posterior update against the fp64 MFMA roofline at SURVEY §8d's n^3/3 flops (the Cholesky; the
+            # L^-T inverse computed for the sweep adds another n^3/3 not counted here): a latency-bound chain of
+            # n/64 dependent panel launches, far from the bound
+            "updates_roofline": {"flops_per_update": n ** 3 / 3.0,
+                                 "achieved": (n ** 3 / 3.0) * P / (fit_elapsed / fit_reps) / 1e12,
+                                 "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                 "frac": (n ** 3 / 3.0) * P / (fit_elapsed / fit_reps) / 1e12 / FP64_PEAK_TFLOPS},
             "best": {"value": float(bv.item()), "index": int(bi.item())},
             "roofline": {
                 "kernel": "trmm_sumsq_kernel (V = L^-1 K*, fp64 MFMA 16x16x4)",
