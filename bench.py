@@ -162,7 +162,8 @@ def cpu_baseline(X, y, Xs_np, kind, acq, ls, sample, reps=3):
 
 def other_configs(eng, dev, seed):
     """Side measurements at N=1 of the other GPU configs of BASELINE.json (not the headline `value`):
-    configs[2] n=16384 d=8 Matern-5/2 posterior update, configs[4] n=4096 d=16 fp32 covariance build + UCB sweep."""
+    configs[2] n=16384 d=8 Matern-5/2 posterior update, configs[4] n=4096 d=16 fp32 covariance build + UCB sweep,
+    and the north star's n = 1024 point (update + EI sweep)."""
     out = {}
     X_np, y_np = synthetic.problem(16384, 8, seed + 7)
     X, y = torch.tensor(X_np, device=dev), torch.tensor(y_np, device=dev)
@@ -201,6 +202,31 @@ def other_configs(eng, dev, seed):
     out["configs[4]"] = {"workload": "n=4096 d=16 RBF, fp32 covariance build, fp64 factorisation, 1048576-candidate "
                                      "UCB sweep + argmax", "ms_per_step": 1e3 * t, "acq_cands_per_s": (1 << 20) / t,
                          "best_index": int(bi.item())}
+    del st, X, y, Xs
+    torch.cuda.empty_cache()
+    # the north star's n = 1k point (n in {1k, 4k, 16k}): posterior update + 2^20-candidate EI sweep + argmax
+    X_np, y_np = synthetic.problem(1024, 8, seed + 13)
+    Xs_np = synthetic.sobol(1 << 20, 8, seed + 14)
+    X, y, Xs = (torch.tensor(v, device=dev) for v in (X_np, y_np, Xs_np))
+    p = KernelParams("rbf", botorch_default_lengthscale(8), noise=1e-4)
+    bf = float(y_np.max())
+    st = eng.fit(X, y, p)
+    eng.acquire(st, Xs, "ei", best_f=bf)
+    tf, ts = [], []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        st = eng.fit(X, y, p, check=False, out=st)
+        torch.cuda.synchronize()
+        b = time.perf_counter()
+        bv, bi = eng.acquire(st, Xs, "ei", best_f=bf)
+        torch.cuda.synchronize()
+        tf.append(b - a)
+        ts.append(time.perf_counter() - a)
+    t, f = float(np.median(ts)), float(np.median(tf))
+    out["n=1024"] = {"workload": "n=1024 d=8 RBF fp64 posterior update + 1048576-candidate EI sweep + argmax",
+                     "fit_ms": 1e3 * f, "updates_per_s": 1.0 / f, "ms_per_step": 1e3 * t,
+                     "acq_cands_per_s": (1 << 20) / t, "best_index": int(bi.item())}
     return out
 
 
@@ -255,13 +281,14 @@ def main():
         step()
     barrier(dist)
     eng.timing_reset()
-    eng.timing_enable(["trmm"])
+    eng.timing_enable(["trmm", "kstar"])
     t0 = time.perf_counter()
     for _ in range(args.steps):
         bv, bi = step()
     barrier(dist)
     elapsed = time.perf_counter() - t0
     trmm_ms, trmm_launches = eng.timing_query("trmm")
+    kstar_ms, kstar_launches = eng.timing_query("kstar")
     eng.timing_disable()
     if any(st.pivot_failure() >= 0 for st in states):
         raise RuntimeError("Cholesky failed inside the benchmark")
@@ -287,6 +314,12 @@ def main():
         cands_per_launch = P * m * args.steps / max(trmm_launches, 1)
         flops_per_launch = float(n) * n * cands_per_launch  # n^2 flops per candidate (v = L^-1 k*)
         achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
+        # kernel build K(X, X*): writes npad x C fp64 per launch, reads X and the chunk's candidates once
+        npad = -(-n // 128) * 128
+        kc = P * m * args.steps / max(kstar_launches, 1)
+        kstar_bytes = 8.0 * (npad * kc + (n + kc) * args.d)
+        kstar_avg = kstar_ms / max(kstar_launches, 1)
+        kstar_gbs = kstar_bytes / (kstar_avg * 1e-3) / 1e9
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(X_np, y_np, Xs_np, args.kernel, args.acq, ls, args.cpu_sample)
@@ -337,6 +370,12 @@ def main():
                 "launches": trmm_launches,
                 "flops_per_launch": flops_per_launch,
             },
+            # the kernel build against the HBM roofline (north star): its write of K* is the algorithmic traffic;
+            # the fp64 exp per element keeps it VALU-bound below the HBM bound
+            "kernel_build_roofline": {"kernel": "kstar_kernel (K(X, X*) for one candidate chunk)", "bound": "hbm",
+                                      "achieved": kstar_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                      "frac": kstar_gbs / HBM_PEAK_GBS, "bytes_per_launch": kstar_bytes,
+                                      "avg_launch_ms": kstar_avg, "launches": kstar_launches},
             "cpu_baseline": cpu,
             "other_configs": extra,
         }
