@@ -323,18 +323,24 @@ __global__ void __launch_bounds__(WG) argmax_final_kernel(const double* __restri
 
 // ---- host side -------------------------------------------------------------------------------------------
 int64_t sweep_chunk_size(int64_t npad, int64_t m) {
-  // K* chunk capped at ~256 MiB (it is re-read (I+1) times by trmm_sumsq; keeping it near the 256 MiB
-  // Infinity Cache helps), at most 16384 candidates, multiple of 256.  GPX_SWEEP_CHUNK_MB overrides the byte
-  // budget (experiments).
+  // K* chunk of at most ~1 GiB and 32768 candidates, multiple of 256 (tools/chunk_sweep.sh at n = 4096: 256 MiB /
+  // 16384 -> 3.74e6, 512 MiB -> 3.78e6, 1 GiB / 32768 -> 3.81e6, 2 GiB / 65536 -> 3.73e6 candidates/s: fewer
+  // launch tails and K* / finalize launches until K* outgrows what the Infinity Cache keeps warm for the trmm
+  // re-reads).  GPX_SWEEP_CHUNK_MB / GPX_SWEEP_CHUNK_MAX override budget and cap (experiments).
   static const int64_t budget_mb = [] {
     const char* e = getenv("GPX_SWEEP_CHUNK_MB");
     const long v = e ? atol(e) : 0;
-    return (int64_t)(v > 0 ? v : 256);
+    return (int64_t)(v > 0 ? v : 1024);
   }();
   int64_t cap = budget_mb * ((int64_t)1 << 20) / 8 / npad;
   cap = (cap / 256) * 256;
   if (cap < 256) cap = 256;
-  if (cap > 16384) cap = 16384;
+  static const int64_t max_cands = [] {
+    const char* e = getenv("GPX_SWEEP_CHUNK_MAX");
+    const long v = e ? atol(e) : 0;
+    return (int64_t)(v > 0 ? v : 32768);
+  }();
+  if (cap > max_cands) cap = max_cands;
   int64_t need = ((m + 255) / 256) * 256;
   if (need < 256) need = 256;
   return need < cap ? need : cap;

@@ -214,21 +214,27 @@ def test_acquire_argmax(engine, acq, kind):
 
 
 def test_acquire_ties_lowest_index_across_chunks(engine):
-    n, d = 4096, 8  # padded 4096 -> sweep chunks of 8192 candidates
+    n, d = 4096, 8  # padded 4096 -> sweep chunks of 32768 candidates (gpx_sweep.hip sweep_chunk_size)
     X, y = O.synthetic_problem(n, d, 31)
     kp, op = pair("rbf", d, noise=1e-4)
     st = engine.fit(t(X), t(y), kp)
-    base = O.sobol_candidates(9000, d, 32)
+    nb = 33000
+    base = O.sobol_candidates(nb, d, 32)
     bv, bi = engine.acquire(st, t(base), "ucb", beta=4.0)
     i0 = int(bi.item())
-    # place exact copies of the winner later in the same chunk and in the next chunk
-    Xs = np.concatenate([base, base[i0:i0 + 1], base[:8000], base[i0:i0 + 1]])
+    # exact copies of the winner at index nb (chunk 1) and 2 nb + 1 (chunk 2)
+    Xs = np.concatenate([base, base[i0:i0 + 1], base[:nb], base[i0:i0 + 1]])
     bv2, bi2 = engine.acquire(st, t(Xs), "ucb", beta=4.0)
     assert int(bi2.item()) == i0 and float(bv2.item()) == float(bv.item())
-    # with the original winner removed, the first copy (index 8999 after removal) must win
+    # with the original winner removed, the first copy (index nb - 1 after removal) must win over its twin
     Xr = np.concatenate([np.delete(base, i0, axis=0), base[i0:i0 + 1], base[i0:i0 + 1]])
     _, bi3 = engine.acquire(st, t(Xr), "ucb", beta=4.0)
-    assert int(bi3.item()) == 8999
+    assert int(bi3.item()) == nb - 1
+    # winner only in the last chunk, twins straddling the chunk boundary at 65536
+    Xb = np.concatenate([np.delete(base, i0, axis=0), np.delete(base, i0, axis=0)[:32536], base[i0:i0 + 1],
+                         base[i0:i0 + 1]])
+    _, bi4 = engine.acquire(st, t(Xb), "ucb", beta=4.0)
+    assert int(bi4.item()) == (nb - 1) + 32536 == 65535
 
 
 def test_index_offset_and_combine(engine):
