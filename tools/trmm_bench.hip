@@ -154,6 +154,57 @@ struct Tile5 : public MfmaTile<T128, T128, BK, true, true> {
     }
   }
 };
+// Tile7: the shipped tile with the next k-tile's LDS writes moved INTO the MFMA stream, after POS of the 4
+// k-substeps (POS = 4 is the shipped order: writes after all MFMAs), last iteration peeled (no runtime branch).
+template <int BK, int POS>
+struct Tile7 : public MfmaTile<T128, T128, BK, true, true> {
+  using B_ = MfmaTile<T128, T128, BK, true, true>;
+  template <bool STORE>
+  __device__ __forceinline__ void compute_store(const double* sA, const double* sB, double* nA, double* nB) {
+    double a0[4], b0[4], a1[4], b1[4];
+    this->frag(sA, sB, 0, a0, b0);
+#pragma unroll
+    for (int ks = 0; ks < BK; ks += 8) {
+      this->frag(sA, sB, ks + 4, a1, b1);
+      this->mm(a0, b0);
+      if (STORE && POS == ks / 4 + 1) this->store_lds(nA, nB);
+      if (ks + 8 < BK) this->frag(sA, sB, ks + 8, a0, b0);
+      this->mm(a1, b1);
+      if (STORE && POS == ks / 4 + 2) this->store_lds(nA, nB);
+    }
+  }
+  __device__ __forceinline__ void run(const double* A, int64_t lda, const double* B, int64_t ldb, int kbeg, int kend,
+                                      double* smem) {
+    this->zero();
+    double* cur = smem;
+    double* nxt = smem + BK * (B_::PA + B_::PB);
+    this->load_regs(A, lda, B, ldb, kbeg);
+    this->store_lds(cur, cur + BK * B_::PA);
+    __syncthreads();
+    int k0 = kbeg;
+    for (; k0 + BK < kend; k0 += BK) {
+      this->load_regs(A, lda, B, ldb, k0 + BK);
+      compute_store<true>(cur, cur + BK * B_::PA, nxt, nxt + BK * B_::PA);
+      __syncthreads();
+      double* tt = cur; cur = nxt; nxt = tt;
+    }
+    compute_store<false>(cur, cur + BK * B_::PA, nxt, nxt + BK * B_::PA);
+    __syncthreads();
+  }
+};
+
+template <class Tile>
+__device__ __forceinline__ void sumsq_epilogue(Tile& tile, double* smem, double* out);
+template <int POS>
+__global__ void __launch_bounds__(WG) v7(const double* W, int64_t ldw, const double* K, int64_t C, int nI, double* ss) {
+  using Tile = Tile7<16, POS>;
+  __shared__ __attribute__((aligned(16))) double smem[Tile::LDS_DOUBLES];
+  const int I = nI - 1 - blockIdx.y, cb = blockIdx.x;
+  Tile tile;
+  tile.run(W + (int64_t)I * T128, ldw, K + (int64_t)cb * T128, C, 0, (I + 1) * T128, smem);
+  sumsq_epilogue(tile, smem, ss + (int64_t)I * C + (int64_t)cb * T128);
+}
+
 // V6: no LDS, no barriers: every wave streams its own A/B fragments straight from L2 into registers,
 // prefetching PF k-substeps ahead.
 template <int PF>
@@ -406,10 +457,10 @@ __global__ void __launch_bounds__(WG) v1(const double* W, int64_t ldw, const dou
 
 int main(int argc, char** argv) {
   const int n = 4096;
-  std::vector<int> Cs = {4096, 8192};
+  std::vector<int> Cs = {8192, 32768};
   const int nI = n / T128;
   double *W, *K, *ss0, *ss1;
-  size_t Cmax = 8192;
+  size_t Cmax = 32768;
   CK(hipMalloc(&W, (size_t)n * n * 8));
   CK(hipMalloc(&K, (size_t)n * Cmax * 8));
   CK(hipMalloc(&ss0, (size_t)nI * Cmax * 8));
@@ -432,14 +483,13 @@ int main(int argc, char** argv) {
     auto run = [&](int which) {
       const int ncb = C / T128;
       if (which == 0) v0<16><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss0);
-      if (which == 1) v5<16, false><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
-      if (which == 2) v6<2><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
-      if (which == 3) v6<4><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
-      if (which == 4) v2<16, 2><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
-      if (which == 5) v4<16><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
+      if (which == 1) v7<1><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
+      if (which == 2) v7<2><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
+      if (which == 3) v7<3><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
+      if (which == 4) v7<4><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
     };
-    const char* names[] = {"v0 heavy-first BK16", "v5 fragdb", "v6 noLDS pf2", "v6 noLDS pf4", "v2 single BK16 lb2", "v4 glds BK16"};
-    const int NV = 6;
+    const char* names[] = {"v0 shipped tile", "v7 store@1", "v7 store@2", "v7 store@3", "v7 store@4(peeled)"};
+    const int NV = 5;
     std::vector<std::vector<float>> t(NV);
     for (int w = 0; w < NV; ++w) run(w);
     CK(hipDeviceSynchronize());
