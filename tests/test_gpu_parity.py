@@ -477,3 +477,34 @@ def test_c_abi_example_program():
     assert os.path.exists(exe), "build the C example with __graft_entry__.build()"
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "capi example ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_empty_and_non_finite_inputs(engine):
+    """Edge inputs: no training points, no candidates, NaN training inputs (a NaN pivot is a failed Cholesky, as
+    psd_safe_cholesky reports it) and NaN candidates (a NaN score never wins the argmax)."""
+    from bayesianoptimizer_amd import GPXError, NotPositiveDefiniteError
+
+    d = 3
+    with pytest.raises((ValueError, GPXError)):
+        engine.fit(t(np.zeros((0, d))), t(np.zeros(0)), KernelParams("rbf", 0.5))
+    X, y = O.synthetic_problem(40, d, 5)
+    kp, op = pair("matern52", d, noise=1e-4)
+    st = engine.fit(t(X), t(y), kp)
+    mu, var = engine.posterior(st, t(np.zeros((0, d))))
+    assert mu.shape == (0, 1) and var.shape == (0,)
+    with pytest.raises(ValueError):
+        engine.acquire(st, t(np.zeros((0, d))), "ei", best_f=float(y.max()))
+    Xn = X.copy()
+    Xn[7, 1] = np.nan
+    with pytest.raises(NotPositiveDefiniteError):
+        engine.fit(t(Xn), t(y), kp)
+    Xs = O.sobol_candidates(500, d, 6)
+    bv, bi, sc = engine.acquire(st, t(Xs), "logei", best_f=float(y.max()), return_scores=True)
+    i0 = int(bi.item())
+    Xs2 = Xs.copy()
+    Xs2[i0, 0] = np.nan  # the winner becomes NaN: the runner-up must win, scores elsewhere unchanged
+    bv2, bi2, sc2 = engine.acquire(st, t(Xs2), "logei", best_f=float(y.max()), return_scores=True)
+    s1, s2 = sc.cpu().numpy(), sc2.cpu().numpy()
+    assert np.isnan(s2[i0]) and np.array_equal(np.delete(s1, i0), np.delete(s2, i0))
+    ref = np.delete(np.arange(500), i0)[int(np.argmax(np.delete(s1, i0)))]
+    assert int(bi2.item()) == ref and float(bv2.item()) == s1[ref]
