@@ -323,10 +323,12 @@ __global__ void __launch_bounds__(WG) argmax_final_kernel(const double* __restri
 
 // ---- host side -------------------------------------------------------------------------------------------
 int64_t sweep_chunk_size(int64_t npad, int64_t m) {
-  // K* chunk of at most ~1 GiB and 32768 candidates, multiple of 256 (tools/chunk_sweep.sh at n = 4096: 256 MiB /
-  // 16384 -> 3.74e6, 512 MiB -> 3.78e6, 1 GiB / 32768 -> 3.81e6, 2 GiB / 65536 -> 3.73e6 candidates/s: fewer
+  // K* chunk of at most ~1 GiB, multiple of 256 candidates (tools/chunk_sweep.sh at n = 4096: 256 MiB / 8192
+  // candidates -> 3.74e6, 512 MiB -> 3.78e6, 1 GiB / 32768 -> 3.81e6, 2 GiB / 65536 -> 3.73e6 candidates/s: fewer
   // launch tails and K* / finalize launches until K* outgrows what the Infinity Cache keeps warm for the trmm
-  // re-reads).  GPX_SWEEP_CHUNK_MB / GPX_SWEEP_CHUNK_MAX override budget and cap (experiments).
+  // re-reads).  The byte budget alone sets small-n chunks (tools/small_n_rates.py, 2^22 candidates: a 32768 cap
+  // left n = 64 / 256 launch-bound at 3.4e8 / 2.5e8 candidates/s, 1.15e9 / 4.4e8 without it).
+  // GPX_SWEEP_CHUNK_MB / GPX_SWEEP_CHUNK_MAX override budget and cap (experiments).
   static const int64_t budget_mb = [] {
     const char* e = getenv("GPX_SWEEP_CHUNK_MB");
     const long v = e ? atol(e) : 0;
@@ -338,7 +340,7 @@ int64_t sweep_chunk_size(int64_t npad, int64_t m) {
   static const int64_t max_cands = [] {
     const char* e = getenv("GPX_SWEEP_CHUNK_MAX");
     const long v = e ? atol(e) : 0;
-    return (int64_t)(v > 0 ? v : 32768);
+    return (int64_t)(v > 0 ? v : (int64_t)1 << 20);
   }();
   if (cap > max_cands) cap = max_cands;
   int64_t need = ((m + 255) / 256) * 256;
