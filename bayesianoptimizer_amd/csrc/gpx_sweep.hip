@@ -87,7 +87,10 @@ __device__ __forceinline__ void load_point(const gpx_kernel_params& p, const dou
 }
 
 // ---- 1. K* and partial means ---------------------------------------------------------------------------
-template <int DMAX, bool F32>
+// KIND and ONE_RHS are compile-time so the per-element loop carries no uniform branches (kind dispatch, nrhs
+// predicates); dimensions k >= d are zero in both sx/sr and xs/xr, so the distance and linear sums run over all DMAX
+// without a k < d test (adding +0 leaves r2 and lv bitwise unchanged).  Rows j >= n of the last block are zero.
+template <int DMAX, bool F32, int KIND, bool ONE_RHS>
 __global__ void __launch_bounds__(WG) kstar_kernel(gpx_kernel_params p, int n, const double* __restrict__ X,
                                                    int64_t ldx, const double* __restrict__ alpha, int nrhs,
                                                    const double* __restrict__ Xs, int64_t ldxs, int64_t m_chunk,
@@ -97,7 +100,6 @@ __global__ void __launch_bounds__(WG) kstar_kernel(gpx_kernel_params p, int n, c
   const int jb = blockIdx.y;
   const int j0 = jb * NB;
   const int d = p.d;
-  const bool lin = (p.kind == GPX_KERNEL_SCALE_LINEAR_MATERN52);
   for (int e = threadIdx.x; e < NB * DMAX; e += WG) {
     const int r = e / DMAX, k = e % DMAX;
     double v = 0.0;
@@ -117,42 +119,42 @@ __global__ void __launch_bounds__(WG) kstar_kernel(gpx_kernel_params p, int n, c
   double mu[GPX_MAX_RHS];
 #pragma unroll
   for (int q = 0; q < GPX_MAX_RHS; ++q) mu[q] = 0.0;
-  for (int j = 0; j < NB; ++j) {
-    double kv = 0.0;
-    if (j0 + j < n) {
-      double lv = 0.0;
-      if (lin) {
+  const int jn = n - j0 < NB ? n - j0 : NB;  // real rows of this block (<= 0 for an all-padding block)
+  int j = 0;
+  for (; j < jn; ++j) {
+    double lv = 0.0;
+    if (KIND == GPX_KERNEL_SCALE_LINEAR_MATERN52) {
 #pragma unroll
-        for (int k = 0; k < DMAX; ++k)
-          if (k < d) lv += sr[j][k] * xr[k];
+      for (int k = 0; k < DMAX; ++k) lv += sr[j][k] * xr[k];
+    }
+    double kv;
+    if (F32) {
+      float r2 = 0.0f;
+#pragma unroll
+      for (int k = 0; k < DMAX; ++k) {
+        const float df = (float)sx[j][k] - (float)xs[k];
+        r2 += df * df;
       }
-      if (F32) {
-        float r2 = 0.0f;
+      kv = cov_from_r2_f32(KIND, p.outputscale, r2, lv);
+    } else {
+      double r2 = 0.0;
 #pragma unroll
-        for (int k = 0; k < DMAX; ++k) {
-          if (k < d) {
-            const float df = (float)sx[j][k] - (float)xs[k];
-            r2 += df * df;
-          }
-        }
-        kv = cov_from_r2_f32(p.kind, p.outputscale, r2, lv);
-      } else {
-        double r2 = 0.0;
-#pragma unroll
-        for (int k = 0; k < DMAX; ++k) {
-          if (k < d) {
-            const double df = sx[j][k] - xs[k];
-            r2 += df * df;
-          }
-        }
-        kv = cov_from_r2(p.kind, p.outputscale, r2, lv);
+      for (int k = 0; k < DMAX; ++k) {
+        const double df = sx[j][k] - xs[k];
+        r2 += df * df;
       }
+      kv = cov_from_r2(KIND, p.outputscale, r2, lv);
     }
     kstar[(int64_t)(j0 + j) * C + c] = kv;
+    if (ONE_RHS) {
+      mu[0] += sa[j][0] * kv;
+    } else {
 #pragma unroll
-    for (int q = 0; q < GPX_MAX_RHS; ++q)
-      if (q < nrhs) mu[q] += sa[j][q] * kv;
+      for (int q = 0; q < GPX_MAX_RHS; ++q)
+        if (q < nrhs) mu[q] += sa[j][q] * kv;
+    }
   }
+  for (; j < NB; ++j) kstar[(int64_t)(j0 + j) * C + c] = 0.0;
   for (int q = 0; q < nrhs; ++q) mu_part[((int64_t)jb * nrhs + q) * C + c] = mu[q];
 }
 
@@ -371,11 +373,16 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
   {
     LaunchTimer tm(c, GPX_TIMER_KSTAR);
     dim3 g(ncb, nJB);
-#define GPX_KSTAR(D)                                                                                               \
-  (p.cov_fp32 ? kstar_kernel<D, true><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk, C,    \
-                                                               b.kstar, b.mu_part)                               \
-              : kstar_kernel<D, false><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk, C,   \
-                                                                b.kstar, b.mu_part))
+#define GPX_KSTAR_K(D, F, K)                                                                                     \
+  (nrhs == 1 ? kstar_kernel<D, F, K, true><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk, C, \
+                                                                    b.kstar, b.mu_part)                            \
+             : kstar_kernel<D, F, K, false><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk, \
+                                                                     C, b.kstar, b.mu_part))
+#define GPX_KSTAR_F(D, F)                                                                                          \
+  (p.kind == GPX_KERNEL_RBF        ? GPX_KSTAR_K(D, F, GPX_KERNEL_RBF)                                             \
+   : p.kind == GPX_KERNEL_MATERN52 ? GPX_KSTAR_K(D, F, GPX_KERNEL_MATERN52)                                        \
+                                   : GPX_KSTAR_K(D, F, GPX_KERNEL_SCALE_LINEAR_MATERN52))
+#define GPX_KSTAR(D) (p.cov_fp32 ? GPX_KSTAR_F(D, true) : GPX_KSTAR_F(D, false))
     if (p.d <= 4)
       GPX_KSTAR(4);
     else if (p.d <= 8)
@@ -385,6 +392,8 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
     else
       GPX_KSTAR(32);
 #undef GPX_KSTAR
+#undef GPX_KSTAR_F
+#undef GPX_KSTAR_K
   }
   {
     LaunchTimer tm(c, GPX_TIMER_TRMM);
@@ -458,8 +467,12 @@ hipError_t launch_svgp_chunk(Context* c, const gpx_kernel_params& p, double min_
   {
     LaunchTimer tm(c, GPX_TIMER_KSTAR);
     dim3 g(ncb, nJB);
-#define GPX_KSTAR(D) kstar_kernel<D, false><<<g, WG, 0, c->stream>>>(p, M, Z, ldz, alpha, 1, Xs, ldxs, m_chunk, C, \
-                                                                      b.kstar, b.mu_part)
+#define GPX_KSTAR_K(D, K) \
+  kstar_kernel<D, false, K, true><<<g, WG, 0, c->stream>>>(p, M, Z, ldz, alpha, 1, Xs, ldxs, m_chunk, C, b.kstar, b.mu_part)
+#define GPX_KSTAR(D)                                                                         \
+  (p.kind == GPX_KERNEL_RBF        ? GPX_KSTAR_K(D, GPX_KERNEL_RBF)                          \
+   : p.kind == GPX_KERNEL_MATERN52 ? GPX_KSTAR_K(D, GPX_KERNEL_MATERN52)                     \
+                                   : GPX_KSTAR_K(D, GPX_KERNEL_SCALE_LINEAR_MATERN52))
     if (p.d <= 4)
       GPX_KSTAR(4);
     else if (p.d <= 8)
@@ -469,6 +482,7 @@ hipError_t launch_svgp_chunk(Context* c, const gpx_kernel_params& p, double min_
     else
       GPX_KSTAR(32);
 #undef GPX_KSTAR
+#undef GPX_KSTAR_K
   }
   {
     LaunchTimer tm(c, GPX_TIMER_TRMM);
