@@ -33,7 +33,7 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 }  // namespace
 
-template <int DMAX>
+template <int DMAX, int KIND>
 __global__ void __launch_bounds__(WG) mll_grad_kernel(gpx_kernel_params p, int n, int npad,
                                                       const double* __restrict__ X, int64_t ldx,
                                                       const double* __restrict__ W, int64_t ldw,
@@ -81,7 +81,11 @@ __global__ void __launch_bounds__(WG) mll_grad_kernel(gpx_kernel_params p, int n
   }
   const double tk = (double)nrhs;
 
-  const int kind = p.kind;
+  // For KIND >= 0 the kind is compile-time and, dimensions k >= d being zero in xi / xj / il, the distance loop needs
+  // no k < d test (the +0 terms leave every sum bitwise unchanged): no uniform branches per element.
+  // KIND < 0: the kind is read at run time (the Scale(Linear + Matern) instantiation: its extra accumulators only fit
+  // two waves per SIMD in this form, 256 vs 286 VGPRs at d = 8).
+  const int kind = KIND >= 0 ? KIND : p.kind;
   const bool lin = (kind == GPX_KERNEL_SCALE_LINEAR_MATERN52);
   const double s = p.outputscale;
   double il[DMAX];
@@ -120,7 +124,7 @@ __global__ void __launch_bounds__(WG) mll_grad_kernel(gpx_kernel_params p, int n
 #pragma unroll
       for (int k = 0; k < DMAX; ++k) {
         q[k] = 0.0;
-        if (k < d) {
+        if (KIND >= 0 || k < d) {
           const double df = (x1[k] - x2[k]) * il[k];
           q[k] = df * df;
           r2 += q[k];
@@ -140,7 +144,7 @@ __global__ void __launch_bounds__(WG) mll_grad_kernel(gpx_kernel_params p, int n
         double lv = 0.0;
 #pragma unroll
         for (int k = 0; k < DMAX; ++k) {
-          if (k < d) {
+          if (k < d) {  // kept: without it the linear kind's accumulators cost the second wave per SIMD
             const double xx = x1[k] * x2[k];
             lv += p.linear_variance[k] * xx;
             gv[k] += G * xx;
@@ -273,14 +277,21 @@ hipError_t launch_mll(Context* c, const gpx_kernel_params& p, int n, int npad, c
   const int tiles = T * (T + 1) / 2;
   const int kc = mll_kchunk(npad);
   const dim3 grid(tiles, (npad + kc - 1) / kc);
+#define GPX_MLL_K(D, K) mll_grad_kernel<D, K><<<grid, WG, 0, c->stream>>>(p, n, npad, X, ldx, W, ldw, alpha, nrhs, kc, part)
+#define GPX_MLL(D)                                                         \
+  (p.kind == GPX_KERNEL_RBF        ? GPX_MLL_K(D, GPX_KERNEL_RBF)          \
+   : p.kind == GPX_KERNEL_MATERN52 ? GPX_MLL_K(D, GPX_KERNEL_MATERN52)     \
+                                   : GPX_MLL_K(D, -1))
   if (p.d <= 4)
-    mll_grad_kernel<4><<<grid, WG, 0, c->stream>>>(p, n, npad, X, ldx, W, ldw, alpha, nrhs, kc, part);
+    GPX_MLL(4);
   else if (p.d <= 8)
-    mll_grad_kernel<8><<<grid, WG, 0, c->stream>>>(p, n, npad, X, ldx, W, ldw, alpha, nrhs, kc, part);
+    GPX_MLL(8);
   else if (p.d <= 16)
-    mll_grad_kernel<16><<<grid, WG, 0, c->stream>>>(p, n, npad, X, ldx, W, ldw, alpha, nrhs, kc, part);
+    GPX_MLL(16);
   else
-    mll_grad_kernel<32><<<grid, WG, 0, c->stream>>>(p, n, npad, X, ldx, W, ldw, alpha, nrhs, kc, part);
+    GPX_MLL(32);
+#undef GPX_MLL
+#undef GPX_MLL_K
   const int64_t rows = (int64_t)tiles * grid.y;
   const int64_t rpb = std::max<int64_t>(64, (rows + 255) / 256);
   const int nb = (int)((rows + rpb - 1) / rpb);

@@ -275,5 +275,9 @@ def test_exact_gp_fit_hyperparameters_gpu_matches_oracle_engine(engine):
                  outcome_transform=Standardize()).fit_hyperparameters("gamma", options=tight)
     g2 = ExactGP(torch.tensor(X), torch.tensor(Y), KernelParams("matern52", 0.5), engine=OracleEngine(),
                  outcome_transform=Standardize()).fit_hyperparameters("gamma", options=tight)
-    assert abs(g1.mll_result.loss - g2.mll_result.loss) <= 1e-9 * (1 + abs(g2.mll_result.loss))
+    # Same optimum, not the same path: the objective and gradient agree to ~1e-12 at equal parameters (the tests
+    # above), but in this flat optimum L-BFGS-B's relative-reduction stop fires at different iterates once the two
+    # paths differ by rounding (observed: 346 vs 408 evaluations, final losses 1e-7 apart on the same engine build
+    # pair), so the end-to-end check is on the optimum's value and location.
+    assert abs(g1.mll_result.loss - g2.mll_result.loss) <= 1e-6 * (1 + abs(g2.mll_result.loss))
     assert np.allclose(g1.params.lengthscales(3), g2.params.lengthscales(3), rtol=1e-3)
