@@ -216,6 +216,84 @@ __global__ void __launch_bounds__(WG) trmm_sumsq_kernel(const double* __restrict
   }
 }
 
+// ---- 1+2 fused, small n (npad <= 256, one output) ----------------------------------------------------------
+// At small n the K* round trip through HBM and the 128-row trmm tiles (whose triangle is at most two tiles deep)
+// cost more than the product (profiles/r01_small_n_rates.log, n = 256: kstar 2.2 + trmm 6.4 ms per 2^22 candidates
+// at 43 TF/s).  Here one wave owns 16 candidates and walks k in steps of 4: each lane evaluates K*[k][c]
+// (k = k0 + lane/16, c = lane%16) straight into the B operand of v_mfma_f64_16x16x4 (no K* buffer), and the A
+// operands W[k][16 ib + lane%16] of the row blocks ib >= k/16 come from L2 (W is npad^2 fp64 <= 512 KiB, shared by
+// every workgroup).  The triangle is walked in 16-row blocks, so the diagonal waste is 1/16 instead of 1/2 of a
+// 128-row tile.  Outputs per candidate: mu (alpha^T K*, no constant mean) and ss = |W^T K*|^2, in the layout of one
+// mu_part / ss_part block so finalize_kernel runs unchanged with nJB = nI = 1.  The summation order differs from the
+// unfused path (both are checked against the oracle at the same tolerance).
+template <int NPAD, int DMAX, int KIND>
+__global__ void __launch_bounds__(WG) sweep_small_kernel(gpx_kernel_params p, int n, const double* __restrict__ X,
+                                                         int64_t ldx, const double* __restrict__ alpha,
+                                                         const double* __restrict__ W, int64_t ldw,
+                                                         const double* __restrict__ Xs, int64_t ldxs, int64_t m_chunk,
+                                                         double* __restrict__ mu_out, double* __restrict__ ss_out) {
+  constexpr int NRB = NPAD / 16;
+  constexpr bool LIN = KIND == GPX_KERNEL_SCALE_LINEAR_MATERN52;
+  __shared__ double sx[NPAD][DMAX], sr[LIN ? NPAD : 1][DMAX], sa[NPAD];
+  const int d = p.d;
+  for (int e = threadIdx.x; e < NPAD * DMAX; e += WG) {
+    const int r = e / DMAX, k = e % DMAX;
+    const double v = (k < d && r < n) ? X[(int64_t)r * ldx + k] : 0.0;
+    sx[r][k] = (k < d) ? v / p.lengthscale[k] : 0.0;
+    if (LIN) sr[r][k] = (k < d) ? v * p.linear_variance[k] : 0.0;
+  }
+  for (int r = threadIdx.x; r < NPAD; r += WG) sa[r] = r < n ? alpha[r] : 0.0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int kr = lane >> 4;
+  const int64_t c = ((int64_t)blockIdx.x * (WG / 64) + w) * 16 + (lane & 15);
+  const bool valid = c < m_chunk;
+  double xs[DMAX], xr[DMAX];
+  load_point<DMAX>(p, Xs + (valid ? c * ldxs : 0), valid, xs, xr);
+  d4 acc[NRB];
+#pragma unroll
+  for (int ib = 0; ib < NRB; ++ib) acc[ib] = (d4){0.0, 0.0, 0.0, 0.0};
+  double mu = 0.0;
+  const double* __restrict__ Wl = W + (int64_t)kr * ldw + (lane & 15);
+#pragma unroll
+  for (int kb = 0; kb < NRB; ++kb) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int k0 = 16 * kb + 4 * ks;
+      const int j = k0 + kr;
+      double r2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < DMAX; ++k) {
+        const double df = sx[j][k] - xs[k];
+        r2 += df * df;
+      }
+      double lv = 0.0;
+      if (LIN) {
+#pragma unroll
+        for (int k = 0; k < DMAX; ++k) lv += sr[j][k] * xr[k];
+      }
+      double kv = cov_from_r2(KIND, p.outputscale, r2, lv);
+      kv = j < n ? kv : 0.0;
+      mu += sa[j] * kv;
+#pragma unroll
+      for (int ib = kb; ib < NRB; ++ib) acc[ib] = mfma16x16x4(Wl[(int64_t)k0 * ldw + 16 * ib], kv, acc[ib]);
+    }
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int ib = 0; ib < NRB; ++ib)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s += acc[ib][r] * acc[ib][r];
+  s += __shfl_xor(s, 16);
+  s += __shfl_xor(s, 32);
+  mu += __shfl_xor(mu, 16);
+  mu += __shfl_xor(mu, 32);
+  if (lane < 16 && valid) {
+    mu_out[c] = mu;
+    ss_out[c] = s;
+  }
+}
+
 // ---- 3. finalize: posterior (mode 0) or acquisition + block argmax (mode 1) ------------------------------
 struct FinalizeArgs {
   gpx_kernel_params p;
@@ -361,6 +439,13 @@ size_t sweep_workspace_bytes(int64_t npad, int64_t nrhs, int64_t m) {
   return b + 256;
 }
 
+// The fused small-n sweep covers npad <= 256, one output, d <= 16 and the fp64 covariance build; the rest takes the
+// K* + trmm path.  GPX_SWEEP_FUSED=0 forces the unfused path (A/B measurements, parity tests of both paths).
+bool sweep_fused_ok(const gpx_kernel_params& p, int npad, int nrhs) {
+  const char* e = getenv("GPX_SWEEP_FUSED");  // read per chunk: tests flip it inside one process
+  return !(e && e[0] == '0') && (npad == 128 || npad == 256) && nrhs == 1 && p.d <= 16 && !p.cov_fp32;
+}
+
 hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
                               const double* W, int64_t ldw, const double* alpha, int nrhs, const double* Xs,
                               int64_t ldxs, int64_t m_chunk, const SweepBuffers& b, int mode,
@@ -368,9 +453,29 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
                               double* mean_out, int64_t ldmean, double* var_out, double* scores_out,
                               int64_t rec_offset, int64_t index_offset) {
   const int64_t C = b.chunk;
-  const int nJB = npad / NB, nI = npad / TT;
+  int nJB = npad / NB, nI = npad / TT;
   const int ncb = (int)((m_chunk + WG - 1) / WG);  // 256-candidate blocks actually used in this chunk
-  {
+  if (sweep_fused_ok(p, npad, nrhs)) {
+    LaunchTimer tm(c, GPX_TIMER_TRMM);
+    const int nwg = (int)((m_chunk + 63) / 64);
+#define GPX_SMALL_K(NP, D, K)                                                                                       \
+  sweep_small_kernel<NP, D, K><<<nwg, WG, 0, c->stream>>>(p, n, X, ldx, alpha, W, ldw, Xs, ldxs, m_chunk, b.mu_part, \
+                                                          b.ss_part)
+#define GPX_SMALL_D(NP, D)                                                                                          \
+  (p.kind == GPX_KERNEL_RBF        ? GPX_SMALL_K(NP, D, GPX_KERNEL_RBF)                                             \
+   : p.kind == GPX_KERNEL_MATERN52 ? GPX_SMALL_K(NP, D, GPX_KERNEL_MATERN52)                                        \
+                                   : GPX_SMALL_K(NP, D, GPX_KERNEL_SCALE_LINEAR_MATERN52))
+#define GPX_SMALL(NP) (p.d <= 4 ? GPX_SMALL_D(NP, 4) : p.d <= 8 ? GPX_SMALL_D(NP, 8) : GPX_SMALL_D(NP, 16))
+    if (npad == 128)
+      GPX_SMALL(128);
+    else
+      GPX_SMALL(256);
+#undef GPX_SMALL
+#undef GPX_SMALL_D
+#undef GPX_SMALL_K
+    nJB = nI = 1;
+  } else {
+    {
     LaunchTimer tm(c, GPX_TIMER_KSTAR);
     dim3 g(ncb, nJB);
 #define GPX_KSTAR_K(D, F, K)                                                                                     \
@@ -399,6 +504,7 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
     LaunchTimer tm(c, GPX_TIMER_TRMM);
     const int ncbt = (int)((m_chunk + TT - 1) / TT);
     trmm_sumsq_kernel<<<ncbt * nI, WG, 0, c->stream>>>(W, ldw, b.kstar, C, nI, ncbt, b.ss_part, 0);
+  }
   }
   {
     LaunchTimer tm(c, GPX_TIMER_ACQ);
