@@ -227,6 +227,56 @@ def other_configs(eng, dev, seed):
     out["n=1024"] = {"workload": "n=1024 d=8 RBF fp64 posterior update + 1048576-candidate EI sweep + argmax",
                      "fit_ms": 1e3 * f, "updates_per_s": 1.0 / f, "ms_per_step": 1e3 * t,
                      "acq_cands_per_s": (1 << 20) / t, "best_index": int(bi.item())}
+    del st, X, y, Xs
+    torch.cuda.empty_cache()
+    # configs[0]'s problem size (n = 256 d = 4 RBF EI, the reference's own CPU case) on the GPU: the fused small-n
+    # sweep (sweep_small_kernel) over 2^20 candidates, plus its posterior update
+    X_np, y_np = synthetic.problem(256, 4, seed + 15)
+    Xs_np = synthetic.sobol(1 << 20, 4, seed + 16)
+    X, y, Xs = (torch.tensor(v, device=dev) for v in (X_np, y_np, Xs_np))
+    p = KernelParams("rbf", botorch_default_lengthscale(4), noise=1e-4)
+    bf = float(y_np.max())
+    st = eng.fit(X, y, p)
+    eng.acquire(st, Xs, "ei", best_f=bf)
+    tf, ts = [], []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        st = eng.fit(X, y, p, check=False, out=st)
+        torch.cuda.synchronize()
+        b = time.perf_counter()
+        bv, bi = eng.acquire(st, Xs, "ei", best_f=bf)
+        torch.cuda.synchronize()
+        tf.append(b - a)
+        ts.append(time.perf_counter() - b)
+    f, s = float(np.median(tf)), float(np.median(ts))
+    out["n=256 (configs[0] size)"] = {
+        "workload": "n=256 d=4 RBF fp64 posterior update; 1048576-candidate EI sweep + argmax (fused small-n sweep)",
+        "fit_ms": 1e3 * f, "updates_per_s": 1.0 / f, "sweep_ms": 1e3 * s, "acq_cands_per_s": (1 << 20) / s,
+        "best_index": int(bi.item())}
+    del st, X, y, Xs
+    torch.cuda.empty_cache()
+    # the BO loop's per-iteration update done incrementally: one new observation appended to an
+    # n = 4096 fit by the bordered Cholesky (gpx_append_f64; the same factor a refit computes, GPU parity tests),
+    # beside the headline's full refit
+    X_np, y_np = synthetic.problem(4097, 8, seed + 17)
+    X, y = torch.tensor(X_np, device=dev), torch.tensor(y_np, device=dev)
+    p = KernelParams("rbf", botorch_default_lengthscale(8), noise=1e-4)
+    base = eng.fit(X[:4096], y[:4096], p, capacity=4224)
+    ta = []
+    for _ in range(7):
+        base.n, base.npad = 4096, eng.padded_n(4096)
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        st = eng.append(base, X, y, check=False)
+        torch.cuda.synchronize()
+        ta.append(time.perf_counter() - a)
+    if st.pivot_failure() >= 0:
+        raise RuntimeError("append Cholesky failed")
+    t = float(np.median(ta))
+    out["incremental n=4096+1"] = {"workload": "append 1 observation to an n=4096 d=8 RBF fit (bordered Cholesky, "
+                                               "L^-T and alpha updated), exact", "update_ms": 1e3 * t,
+                                   "updates_per_s": 1.0 / t}
     return out
 
 
