@@ -155,8 +155,9 @@ const char* gpx_last_error(gpx_handle h) {
   return c->last_error.c_str();
 }
 
-gpx_status gpx_gram_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
-                        double* K, int64_t ldk) {
+// gram_impl clears *info (when given) inside the gram kernel: the fit needs no separate memset dispatch
+static gpx_status gram_impl(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                            double* K, int64_t ldk, int32_t* info) {
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return GPX_INVALID_ARG;
   GPX_TRY(check_params(c, p));
@@ -167,10 +168,16 @@ gpx_status gpx_gram_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, con
   GPX_TRY(check_ld(c, ldx, p->d, "X", false));
   GPX_TRY(check_ld(c, ldk, npad, "K", true));
   GPX_TRY(use_device(c));
-  return hip_check(c, gpx::launch_gram(c, *p, (int)n, (int)npad, X, ldx, K, ldk), "gram");
+  return hip_check(c, gpx::launch_gram(c, *p, (int)n, (int)npad, X, ldx, K, ldk, gpx::Batch(), 0, info), "gram");
 }
 
-gpx_status gpx_potrf_f64(gpx_handle h, int64_t n, double* A, int64_t lda, double* Dinv, int32_t* info) {
+gpx_status gpx_gram_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                        double* K, int64_t ldk) {
+  return gram_impl(h, p, n, X, ldx, K, ldk, nullptr);
+}
+
+static gpx_status potrf_impl(gpx_handle h, int64_t n, double* A, int64_t lda, double* Dinv, int32_t* info,
+                             bool clear_info) {
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return GPX_INVALID_ARG;
   GPX_TRY(check_n(c, n));
@@ -180,8 +187,12 @@ gpx_status gpx_potrf_f64(gpx_handle h, int64_t n, double* A, int64_t lda, double
   const int64_t npad = padded(n);
   GPX_TRY(check_ld(c, lda, npad, "A", true));
   GPX_TRY(use_device(c));
-  GPX_TRY(hip_check(c, hipMemsetAsync(info, 0, sizeof(int32_t), c->stream), "memset info"));
+  if (clear_info) GPX_TRY(hip_check(c, hipMemsetAsync(info, 0, sizeof(int32_t), c->stream), "memset info"));
   return hip_check(c, gpx::launch_potrf(c, (int)npad, A, lda, Dinv, info), "potrf");
+}
+
+gpx_status gpx_potrf_f64(gpx_handle h, int64_t n, double* A, int64_t lda, double* Dinv, int32_t* info) {
+  return potrf_impl(h, n, A, lda, Dinv, info, true);
 }
 
 gpx_status gpx_trtri_workspace_size(int64_t n, size_t* bytes) {
@@ -251,8 +262,9 @@ gpx_status gpx_fit_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, cons
   if (gpx_fit_workspace_size(n, nrhs, &need) != GPX_OK)
     return fail(c, GPX_INVALID_ARG, "invalid n / nrhs for fit");
   if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "fit workspace too small");
-  GPX_TRY(gpx_gram_f64(h, p, n, X, ldx, K, ldk));
-  GPX_TRY(gpx_potrf_f64(h, n, K, ldk, Dinv, info));
+  if (!info) return fail(c, GPX_INVALID_ARG, "info is NULL");
+  GPX_TRY(gram_impl(h, p, n, X, ldx, K, ldk, info));
+  GPX_TRY(potrf_impl(h, n, K, ldk, Dinv, info, false));
   GPX_TRY(gpx_trtri_f64(h, n, K, ldk, Dinv, W, ldw, ws, ws_bytes));
   return gpx_alpha_f64(h, n, W, ldw, Y, ldy, nrhs, p->const_mean, alpha, ws, ws_bytes);
 }
@@ -375,8 +387,8 @@ gpx_status gpx_fit_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t
   bt.alpha = stride_alpha;
   bt.ws = (int64_t)(fit_slice_bytes(npad, nrhs) / sizeof(double));
   double* slice = align256(ws);
-  GPX_TRY(hip_check(c, hipMemsetAsync(info, 0, sizeof(int32_t) * batch, c->stream), "memset info"));
-  GPX_TRY(hip_check(c, gpx::launch_gram(c, *p, (int)n, (int)npad, X, ldx, K, ldk, bt), "gram"));
+  // the gram kernel clears info[0 .. batch) before the Cholesky (no separate memset dispatch)
+  GPX_TRY(hip_check(c, gpx::launch_gram(c, *p, (int)n, (int)npad, X, ldx, K, ldk, bt, 0, info), "gram"));
   GPX_TRY(hip_check(c, gpx::launch_potrf(c, (int)npad, K, ldk, Dinv, info, bt), "potrf"));
   GPX_TRY(hip_check(c, gpx::launch_trtri(c, (int)npad, K, ldk, Dinv, W, ldw, slice, bt), "trtri"));
   double* zpart = slice;

@@ -14,7 +14,10 @@ namespace gpx {
 template <int DMAX, bool F32>
 __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, int t0, const double* __restrict__ X,
                                                   int64_t ldx, double* __restrict__ K, int64_t ldk, int64_t sx,
-                                                  int64_t sk) {
+                                                  int64_t sk, int32_t* __restrict__ info) {
+  // the fit's pivot-failure word is cleared here (stream-ordered before the Cholesky) instead of by a separate
+  // memset dispatch (~4.7 us at small n)
+  if (info && blockIdx.x == 0 && blockIdx.z == 0 && threadIdx.x == 0) info[blockIdx.y] = 0;
   X += blockIdx.y * sx;  // problem of a batched fit
   K += blockIdx.y * sk;
   __shared__ double si[NB][DMAX + 1], sj[NB][DMAX + 1];    // scaled x / l
@@ -47,7 +50,9 @@ __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, in
     rc[k] = rj[c][k];
   }
   const double diag_add = p.noise + p.jitter;
-  for (int r = threadIdx.x >> 6; r < NB; r += 4) {
+  // gridDim.z row slices per tile (small fits: more workgroups, fewer serial exp chains per thread)
+  const int rows = NB / gridDim.z, rbeg = blockIdx.z * rows;
+  for (int r = rbeg + (threadIdx.x >> 6); r < rbeg + rows; r += 4) {
     const int gi = i0 + r;
     double v;
     if (gi < n && gj < n) {
@@ -87,14 +92,16 @@ __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, in
 }
 
 hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
-                       double* K, int64_t ldk, const Batch& bt, int rb0) {
+                       double* K, int64_t ldk, const Batch& bt, int rb0, int32_t* info) {
   LaunchTimer tm(c, GPX_TIMER_GRAM);
   const int nblk = npad / NB;
   const int t0 = rb0 * (rb0 + 1) / 2;  // tiles of the row blocks above rb0 are skipped (gpx_append_f64)
-  const dim3 grid(nblk * (nblk + 1) / 2 - t0, bt.count);
-#define GPX_GRAM(D)                                                                                       \
-  (p.cov_fp32 ? gram_kernel<D, true><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k) \
-              : gram_kernel<D, false><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k))
+  const int tiles = (nblk * (nblk + 1) / 2 - t0) * bt.count;
+  // fewer tiles than CUs: split each tile's 64 rows over 4 workgroups (n = 128: 11 -> see DESIGN §5)
+  const dim3 grid(nblk * (nblk + 1) / 2 - t0, bt.count, tiles < 256 ? 4 : 1);
+#define GPX_GRAM(D)                                                                                              \
+  (p.cov_fp32 ? gram_kernel<D, true><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info) \
+              : gram_kernel<D, false><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info))
   if (p.d <= 4)
     GPX_GRAM(4);
   else if (p.d <= 8)

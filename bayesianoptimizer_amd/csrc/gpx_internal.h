@@ -53,7 +53,7 @@ struct Batch {
 
 // ---- launch wrappers (defined in the .hip files) -------------------------------------------------
 hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
-                       double* K, int64_t ldk, const Batch& bt = Batch(), int rb0 = 0);
+                       double* K, int64_t ldk, const Batch& bt = Batch(), int rb0 = 0, int32_t* info = nullptr);
 hipError_t launch_potrf(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info,
                         const Batch& bt = Batch());
 hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, const double* Dinv, double* W,

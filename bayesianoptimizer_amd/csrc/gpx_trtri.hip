@@ -146,15 +146,15 @@ __global__ void __launch_bounds__(WG) alpha_z_kernel(int n, int npad, const doub
   W += blockIdx.z * sw;  // problem of a batched fit
   Y += blockIdx.z * sy;
   zpart += blockIdx.z * sws;
-  __shared__ double ys[AK][GPX_MAX_RHS];
+  __shared__ double ys[AK + 16][GPX_MAX_RHS];  // zero rows past the chunk: the last 16-group reads up to AK + 15
   const int i = blockIdx.x * WG + threadIdx.x;
   const int kc = blockIdx.y;
   const int k0 = kc * AK;
   if (k0 > blockIdx.x * WG + WG - 1) return;  // whole chunk below every column of this block: unused
-  for (int e = threadIdx.x; e < AK * nrhs; e += WG) {
-    const int kk = e / nrhs, r = e % nrhs;
+  for (int e = threadIdx.x; e < (AK + 16) * GPX_MAX_RHS; e += WG) {
+    const int kk = e / GPX_MAX_RHS, r = e % GPX_MAX_RHS;
     const int k = k0 + kk;
-    ys[kk][r] = (k < n) ? (Y[(int64_t)k * ldy + r] - const_mean) : 0.0;
+    ys[kk][r] = (kk < AK && r < nrhs && k < n) ? (Y[(int64_t)k * ldy + r] - const_mean) : 0.0;
   }
   __syncthreads();
   double acc[GPX_MAX_RHS];
@@ -162,11 +162,29 @@ __global__ void __launch_bounds__(WG) alpha_z_kernel(int n, int npad, const doub
   for (int r = 0; r < GPX_MAX_RHS; ++r) acc[r] = 0.0;
   if (i < npad) {
     const int kend = min(k0 + AK, i + 1);
-    for (int k = k0; k < kend; ++k) {
-      const double w = W[(int64_t)k * ldw + i];
+    // Branch-free groups of 16: clamped (always in-bounds) W loads, masked to 0 past the column's last row, so the
+    // loads issue together and no per-element branch splits the loop (the per-element `if` form spent 17-23 us in
+    // branches and waits at n = 128).  Accumulation order per output is k ascending, as before; the masked tail
+    // adds +0.0.
+    for (int k = k0; k < kend; k += 16) {
+      double wv[16];
 #pragma unroll
-      for (int r = 0; r < GPX_MAX_RHS; ++r)
-        if (r < nrhs) acc[r] += w * ys[k - k0][r];
+      for (int q = 0; q < 16; ++q) {
+        const int kq = min(k + q, kend - 1);
+        const double v = W[(int64_t)kq * ldw + i];
+        wv[q] = (k + q < kend) ? v : 0.0;
+      }
+      if (nrhs == 1) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[0] += wv[q] * ys[k + q - k0][0];
+      } else {
+#pragma unroll
+        for (int r = 0; r < GPX_MAX_RHS; ++r)
+          if (r < nrhs) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) acc[r] += wv[q] * ys[k + q - k0][r];
+          }
+      }
     }
     for (int r = 0; r < nrhs; ++r) zpart[((int64_t)kc * npad + i) * nrhs + r] = acc[r];
   }
@@ -188,7 +206,7 @@ __global__ void __launch_bounds__(WG) alpha_zsum_kernel(int npad, int nrhs, cons
 // alpha[k][r] = sum_{i >= k} W[k][i] z[i][r]; one wave per row k.
 __global__ void __launch_bounds__(WG) alpha_w_kernel(int n, int npad, const double* __restrict__ W, int64_t ldw,
                                                      const double* __restrict__ z, int nrhs, double* __restrict__ alpha,
-                                                     int64_t sw, int64_t sws, int64_t sa) {
+                                                     int64_t sw, int64_t sws, int64_t sa, int zfold = 0) {
   W += blockIdx.y * sw;
   z += blockIdx.y * sws;
   alpha += blockIdx.y * sa;
@@ -201,8 +219,18 @@ __global__ void __launch_bounds__(WG) alpha_w_kernel(int n, int npad, const doub
   for (int i = k + lane; i < npad; i += 64) {
     const double w = W[(int64_t)k * ldw + i];
 #pragma unroll
-    for (int r = 0; r < GPX_MAX_RHS; ++r)
-      if (r < nrhs) acc[r] += w * z[(int64_t)i * nrhs + r];
+    for (int r = 0; r < GPX_MAX_RHS; ++r) {
+      if (r < nrhs) {
+        double zi;
+        if (zfold) {  // z = the zpart chunk sums, in alpha_zsum_kernel's order (small npad: one dispatch fewer)
+          zi = 0.0;
+          for (int kc = 0; kc * AK <= i; ++kc) zi += z[(int64_t)kc * npad * nrhs + (int64_t)i * nrhs + r];
+        } else {
+          zi = z[(int64_t)i * nrhs + r];
+        }
+        acc[r] += w * zi;
+      }
+    }
   }
 #pragma unroll
   for (int r = 0; r < GPX_MAX_RHS; ++r) {
@@ -219,6 +247,11 @@ hipError_t launch_alpha(Context* c, int n, int npad, const double* W, int64_t ld
   LaunchTimer tm(c, GPX_TIMER_ALPHA);
   dim3 g1((npad + WG - 1) / WG, npad / AK, bt.count);
   alpha_z_kernel<<<g1, WG, 0, c->stream>>>(n, npad, W, ldw, Y, ldy, nrhs, const_mean, zpart, bt.w, bt.y, bt.ws);
+  if (npad <= 4 * AK) {  // <= 4 chunks: alpha_w sums them itself (z entries re-read per row, from L2)
+    alpha_w_kernel<<<dim3((npad + 3) / 4, bt.count), WG, 0, c->stream>>>(n, npad, W, ldw, zpart, nrhs, alpha, bt.w,
+                                                                          bt.ws, bt.alpha, 1);
+    return hipGetLastError();
+  }
   alpha_zsum_kernel<<<dim3((npad * nrhs + WG - 1) / WG, bt.count), WG, 0, c->stream>>>(npad, nrhs, zpart, z, bt.ws);
   alpha_w_kernel<<<dim3((npad + 3) / 4, bt.count), WG, 0, c->stream>>>(n, npad, W, ldw, z, nrhs, alpha, bt.w, bt.ws,
                                                                         bt.alpha);
