@@ -177,7 +177,7 @@ gpx_status gpx_gram_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, con
 }
 
 static gpx_status potrf_impl(gpx_handle h, int64_t n, double* A, int64_t lda, double* Dinv, int32_t* info,
-                             bool clear_info) {
+                             bool clear_info, double* W = nullptr, int64_t ldw = 0) {
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return GPX_INVALID_ARG;
   GPX_TRY(check_n(c, n));
@@ -188,7 +188,7 @@ static gpx_status potrf_impl(gpx_handle h, int64_t n, double* A, int64_t lda, do
   GPX_TRY(check_ld(c, lda, npad, "A", true));
   GPX_TRY(use_device(c));
   if (clear_info) GPX_TRY(hip_check(c, hipMemsetAsync(info, 0, sizeof(int32_t), c->stream), "memset info"));
-  return hip_check(c, gpx::launch_potrf(c, (int)npad, A, lda, Dinv, info), "potrf");
+  return hip_check(c, gpx::launch_potrf(c, (int)npad, A, lda, Dinv, info, gpx::Batch(), W, ldw), "potrf");
 }
 
 gpx_status gpx_potrf_f64(gpx_handle h, int64_t n, double* A, int64_t lda, double* Dinv, int32_t* info) {
@@ -201,8 +201,8 @@ gpx_status gpx_trtri_workspace_size(int64_t n, size_t* bytes) {
   return GPX_OK;
 }
 
-gpx_status gpx_trtri_f64(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv, double* W,
-                         int64_t ldw, void* ws, size_t ws_bytes) {
+static gpx_status trtri_impl(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv, double* W,
+                             int64_t ldw, void* ws, size_t ws_bytes, bool diag_done) {
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return GPX_INVALID_ARG;
   GPX_TRY(check_n(c, n));
@@ -215,7 +215,13 @@ gpx_status gpx_trtri_f64(gpx_handle h, int64_t n, const double* L, int64_t ldl, 
   GPX_TRY(check_ld(c, ldw, npad, "W", true));
   if (ws_bytes < trtri_ws(npad)) return fail(c, GPX_INVALID_ARG, "trtri workspace too small");
   GPX_TRY(use_device(c));
-  return hip_check(c, gpx::launch_trtri(c, (int)npad, L, ldl, Dinv, W, ldw, align256(ws)), "trtri");
+  return hip_check(c, gpx::launch_trtri(c, (int)npad, L, ldl, Dinv, W, ldw, align256(ws), gpx::Batch(), diag_done),
+                   "trtri");
+}
+
+gpx_status gpx_trtri_f64(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv, double* W,
+                         int64_t ldw, void* ws, size_t ws_bytes) {
+  return trtri_impl(h, n, L, ldl, Dinv, W, ldw, ws, ws_bytes, false);
 }
 
 gpx_status gpx_alpha_workspace_size(int64_t n, int64_t nrhs, size_t* bytes) {
@@ -264,8 +270,11 @@ gpx_status gpx_fit_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, cons
   if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "fit workspace too small");
   if (!info) return fail(c, GPX_INVALID_ARG, "info is NULL");
   GPX_TRY(gram_impl(h, p, n, X, ldx, K, ldk, info));
-  GPX_TRY(potrf_impl(h, n, K, ldk, Dinv, info, false));
-  GPX_TRY(gpx_trtri_f64(h, n, K, ldk, Dinv, W, ldw, ws, ws_bytes));
+  if (!W) return fail(c, GPX_INVALID_ARG, "W is NULL");
+  // W's leading dimension is validated before the Dinv pass writes W's diagonal blocks
+  GPX_TRY(check_ld(c, ldw, padded(n), "W", true));
+  GPX_TRY(potrf_impl(h, n, K, ldk, Dinv, info, false, W, ldw));
+  GPX_TRY(trtri_impl(h, n, K, ldk, Dinv, W, ldw, ws, ws_bytes, true));
   return gpx_alpha_f64(h, n, W, ldw, Y, ldy, nrhs, p->const_mean, alpha, ws, ws_bytes);
 }
 
@@ -389,8 +398,8 @@ gpx_status gpx_fit_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t
   double* slice = align256(ws);
   // the gram kernel clears info[0 .. batch) before the Cholesky (no separate memset dispatch)
   GPX_TRY(hip_check(c, gpx::launch_gram(c, *p, (int)n, (int)npad, X, ldx, K, ldk, bt, 0, info), "gram"));
-  GPX_TRY(hip_check(c, gpx::launch_potrf(c, (int)npad, K, ldk, Dinv, info, bt), "potrf"));
-  GPX_TRY(hip_check(c, gpx::launch_trtri(c, (int)npad, K, ldk, Dinv, W, ldw, slice, bt), "trtri"));
+  GPX_TRY(hip_check(c, gpx::launch_potrf(c, (int)npad, K, ldk, Dinv, info, bt, W, ldw), "potrf"));
+  GPX_TRY(hip_check(c, gpx::launch_trtri(c, (int)npad, K, ldk, Dinv, W, ldw, slice, bt, true), "trtri"));
   double* zpart = slice;
   double* z = zpart + (size_t)(npad / 128) * npad * nrhs;
   return hip_check(c, gpx::launch_alpha(c, (int)n, (int)npad, W, ldw, Y, ldy, (int)nrhs, p->const_mean, alpha, zpart, z,

@@ -54,10 +54,12 @@ struct Batch {
 // ---- launch wrappers (defined in the .hip files) -------------------------------------------------
 hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
                        double* K, int64_t ldk, const Batch& bt = Batch(), int rb0 = 0, int32_t* info = nullptr);
+// W (optional): the Dinv pass also writes W's diagonal blocks D_k^T (what trtri_diag would), so a fit that follows
+// with launch_trtri(..., diag_done = true) saves one dispatch.
 hipError_t launch_potrf(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info,
-                        const Batch& bt = Batch());
+                        const Batch& bt = Batch(), double* W = nullptr, int64_t ldw = 0);
 hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, const double* Dinv, double* W,
-                        int64_t ldw, double* T, const Batch& bt = Batch());
+                        int64_t ldw, double* T, const Batch& bt = Batch(), bool diag_done = false);
 hipError_t launch_alpha(Context* c, int n, int npad, const double* W, int64_t ldw, const double* Y, int64_t ldy,
                         int nrhs, double const_mean, double* alpha, double* zpart, double* z,
                         const Batch& bt = Batch());

@@ -299,7 +299,8 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, int lazy
 // L_kk from the scratch into A, and D_k = L_kk^{-1} into the first half of Dinv (one workgroup per block).
 __global__ void __launch_bounds__(WG) potrf_dinv_kernel(double* __restrict__ A, int64_t lda, int nblk,
                                                         double* __restrict__ Dinv, const int32_t* __restrict__ info,
-                                                        int64_t sa, int64_t sd, int k0) {
+                                                        int64_t sa, int64_t sd, int k0, double* __restrict__ W,
+                                                        int64_t ldw, int64_t sw) {
   A += blockIdx.y * sa;
   Dinv += blockIdx.y * sd;
   info += blockIdx.y;
@@ -322,6 +323,15 @@ __global__ void __launch_bounds__(WG) potrf_dinv_kernel(double* __restrict__ A, 
   trinv64(sL, sX, sT);
   double* D = Dinv + (int64_t)k * NB * NB;
   for (int e = t; e < NB * NB; e += WG) D[e] = sX[(e >> 6) * LD64 + (e & 63)];
+  if (W) {  // trtri_diag's work for a fit: W_kk = D_k^T, and the strictly-lower 64-block of an odd 128-tile zeroed
+    W += blockIdx.y * sw;
+    double* Wkk = W + (int64_t)k * NB * ldw + (int64_t)k * NB;
+    for (int e = t; e < NB * NB; e += WG) Wkk[(int64_t)(e >> 6) * ldw + (e & 63)] = sX[(e & 63) * LD64 + (e >> 6)];
+    if (k & 1) {
+      double* Z = W + (int64_t)k * NB * ldw + (int64_t)(k - 1) * NB;
+      for (int e = t; e < NB * NB; e += WG) Z[(int64_t)(e >> 6) * ldw + (e & 63)] = 0.0;
+    }
+  }
 }
 
 // Trailing updates are flushed every `lazy` launches (K = 64 lazy per flush): C tiles are read and written once per
@@ -368,15 +378,17 @@ static void launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double*
 }
 
 static void launch_dinv(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
-                        int k0, int k1) {
-  potrf_dinv_kernel<<<dim3(k1 - k0, bt.count), WG, 0, ctx->stream>>>(A, lda, nblk, Dinv, info, bt.k, bt.dinv, k0);
+                        int k0, int k1, double* W = nullptr, int64_t ldw = 0) {
+  potrf_dinv_kernel<<<dim3(k1 - k0, bt.count), WG, 0, ctx->stream>>>(A, lda, nblk, Dinv, info, bt.k, bt.dinv, k0, W, ldw,
+                                                                      bt.w);
 }
 
-hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt) {
+hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
+                        double* W, int64_t ldw) {
   LaunchTimer tm(ctx, GPX_TIMER_POTRF);
   const int nblk = npad / NB;
   launch_steps(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk);
-  launch_dinv(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk);
+  launch_dinv(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, W, ldw);
   return hipGetLastError();
 }
 

@@ -110,10 +110,10 @@ __global__ void __launch_bounds__(WG) trtri_w_kernel(double* __restrict__ W, int
 }
 
 hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, const double* Dinv, double* W,
-                        int64_t ldw, double* T, const Batch& bt) {
+                        int64_t ldw, double* T, const Batch& bt, bool diag_done) {
   LaunchTimer tm(c, GPX_TIMER_TRTRI);
   const int nblk = npad / NB;
-  trtri_diag_kernel<<<dim3(nblk, bt.count), WG, 0, c->stream>>>(Dinv, W, ldw, bt.dinv, bt.w);
+  if (!diag_done) trtri_diag_kernel<<<dim3(nblk, bt.count), WG, 0, c->stream>>>(Dinv, W, ldw, bt.dinv, bt.w);
   for (int h = 1; h < nblk; h *= 2) {
     const int groups = (nblk + 2 * h - 1) / (2 * h);
     // 128x128 tiles (half the operand traffic per flop) once a level still fills the chip with them: >= 512 paired
