@@ -401,6 +401,89 @@ __device__ __forceinline__ void sumsq_epilogue(Tile& tile, double* smem, double*
   __syncthreads();
 }
 
+// V8: two k-tiles of global prefetch (Tensile's PGR2): the loads of tile t+2 are issued while tile t computes and
+// tile t+1's registers are stored, so a load has two compute windows to land (MALL-hit latency ~1-2 us).  Loop
+// unrolled by two so the two register staging sets alternate statically.
+template <int TM, int TN, int BK>
+struct TilePgr2 : public MfmaTile<TM, TN, BK, true, true> {
+  using Bs = MfmaTile<TM, TN, BK, true, true>;
+  double2 xa[Bs::A_LOADS], xb[Bs::B_LOADS], ya[Bs::A_LOADS], yb[Bs::B_LOADS];
+  template <int NA, int NB_>
+  __device__ __forceinline__ void ld(double2 (&ra)[NA], double2 (&rb)[NB_], const double* __restrict__ A, int64_t lda,
+                                     const double* __restrict__ B, int64_t ldb, int k0) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+      const int e = (t + q * WG) * 2, kk = e / TM, mm = e % TM;
+      ra[q] = *reinterpret_cast<const double2*>(A + (int64_t)(k0 + kk) * lda + mm);
+    }
+#pragma unroll
+    for (int q = 0; q < NB_; ++q) {
+      const int e = (t + q * WG) * 2, kk = e / TN, nn = e % TN;
+      rb[q] = *reinterpret_cast<const double2*>(B + (int64_t)(k0 + kk) * ldb + nn);
+    }
+  }
+  template <int NA, int NB_>
+  __device__ __forceinline__ void st(const double2 (&ra)[NA], const double2 (&rb)[NB_], double* sA, double* sB) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+      const int e = (t + q * WG) * 2, kk = e / TM, mm = e % TM;
+      *reinterpret_cast<double2*>(sA + kk * Bs::PA + mm) = ra[q];
+    }
+#pragma unroll
+    for (int q = 0; q < NB_; ++q) {
+      const int e = (t + q * WG) * 2, kk = e / TN, nn = e % TN;
+      *reinterpret_cast<double2*>(sB + kk * Bs::PB + nn) = rb[q];
+    }
+  }
+  __device__ __forceinline__ void run(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
+                                      int64_t ldb, int kbeg, int kend, double* smem) {
+    this->zero();
+    const int nk = (kend - kbeg) / BK;
+    if (nk <= 0) return;
+    double* cur = smem;
+    double* nxt = smem + BK * (Bs::PA + Bs::PB);
+    ld(xa, xb, A, lda, B, ldb, kbeg);
+    st(xa, xb, cur, cur + BK * Bs::PA);
+    __syncthreads();
+    if (nk > 1) ld(xa, xb, A, lda, B, ldb, kbeg + BK);
+    for (int t = 0; t < nk; t += 2) {
+      if (t + 2 < nk) ld(ya, yb, A, lda, B, ldb, kbeg + (t + 2) * BK);
+      this->compute(cur, cur + BK * Bs::PA);
+      if (t + 1 < nk) st(xa, xb, nxt, nxt + BK * Bs::PA);
+      __syncthreads();
+      { double* q = cur; cur = nxt; nxt = q; }
+      if (t + 1 >= nk) break;
+      if (t + 3 < nk) ld(xa, xb, A, lda, B, ldb, kbeg + (t + 3) * BK);
+      this->compute(cur, cur + BK * Bs::PA);
+      if (t + 2 < nk) st(ya, yb, nxt, nxt + BK * Bs::PA);
+      __syncthreads();
+      { double* q = cur; cur = nxt; nxt = q; }
+    }
+  }
+};
+
+template <int BK>
+__global__ void __launch_bounds__(WG) v9(const double* W, int64_t ldw, const double* K, int64_t C, int nI, double* ss) {
+  using Tile = TilePgr2<T128, T128, BK>;
+  __shared__ __attribute__((aligned(16))) double smem[Tile::LDS_DOUBLES];
+  const int I = nI - 1 - blockIdx.y, cb = blockIdx.x;
+  Tile tile;
+  tile.run(W + (int64_t)I * T128, ldw, K + (int64_t)cb * T128, C, 0, (I + 1) * T128, smem);
+  sumsq_epilogue(tile, smem, ss + (int64_t)I * C + (int64_t)cb * T128);
+}
+
+template <int BK>
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2))) v8(const double* W, int64_t ldw, const double* K, int64_t C, int nI, double* ss) {
+  using Tile = TilePgr2<T128, T128, BK>;
+  __shared__ __attribute__((aligned(16))) double smem[Tile::LDS_DOUBLES];
+  const int I = nI - 1 - blockIdx.y, cb = blockIdx.x;
+  Tile tile;
+  tile.run(W + (int64_t)I * T128, ldw, K + (int64_t)cb * T128, C, 0, (I + 1) * T128, smem);
+  sumsq_epilogue(tile, smem, ss + (int64_t)I * C + (int64_t)cb * T128);
+}
+
 // V0: the shipped kernel (heavy-first row tiles)
 template <int BK>
 __global__ void __launch_bounds__(WG) v0(const double* W, int64_t ldw, const double* K, int64_t C, int nI, double* ss) {
@@ -483,13 +566,12 @@ int main(int argc, char** argv) {
     auto run = [&](int which) {
       const int ncb = C / T128;
       if (which == 0) v0<16><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss0);
-      if (which == 1) v7<1><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
-      if (which == 2) v7<2><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
-      if (which == 3) v7<3><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
-      if (which == 4) v7<4><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
+      if (which == 1) v8<16><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
+      if (which == 2) v9<16><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
+      if (which == 3) v0<16><<<dim3(ncb, nI), WG>>>(W, n, K, C, nI, ss1);
     };
-    const char* names[] = {"v0 shipped tile", "v7 store@1", "v7 store@2", "v7 store@3", "v7 store@4(peeled)"};
-    const int NV = 5;
+    const char* names[] = {"v0 shipped tile", "v8 pgr2 2w/SIMD spill", "v9 pgr2 1w/SIMD", "v0 shipped (again)"};
+    const int NV = 4;
     std::vector<std::vector<float>> t(NV);
     for (int w = 0; w < NV; ++w) run(w);
     CK(hipDeviceSynchronize());
