@@ -440,7 +440,10 @@ size_t sweep_workspace_bytes(int64_t npad, int64_t nrhs, int64_t m) {
 }
 
 // The fused small-n sweep covers npad <= 256, one output, d <= 16 and the fp64 covariance build; the rest takes the
-// K* + trmm path.  GPX_SWEEP_FUSED=0 forces the unfused path (A/B measurements, parity tests of both paths).
+// K* + trmm path.  An npad = 384 instance (d <= 8, 226 VGPRs, 2 waves/SIMD) measured slower than the K* + trmm path
+// (2.20e8 vs 2.66e8 candidates/s at n = 384, profiles/r01_small_n_rates.log): 24 row blocks of A operands per k-step
+// from L2 and half the occupancy of the npad = 256 instance.  GPX_SWEEP_FUSED=0 forces the unfused path (A/B
+// measurements, parity tests of both paths).
 bool sweep_fused_ok(const gpx_kernel_params& p, int npad, int nrhs) {
   const char* e = getenv("GPX_SWEEP_FUSED");  // read per chunk: tests flip it inside one process
   return !(e && e[0] == '0') && (npad == 128 || npad == 256) && nrhs == 1 && p.d <= 16 && !p.cov_fp32;

@@ -1,5 +1,5 @@
-"""Fused small-n sweep (sweep_small_kernel: npad <= 256, one output, d <= 16, fp64 covariance build): every case is
-checked against the oracle at the parity tolerances of tests/test_gpu_parity.py, and against the unfused K* + trmm path
+"""Fused small-n sweep (sweep_small_kernel: npad <= 256, one output, d <= 16, fp64 covariance build; n = 257..384
+cases check the boundary, where both sides take the K* + trmm path): every case is checked against the oracle at the parity tolerances of tests/test_gpu_parity.py, and against the unfused K* + trmm path
 of the same library (GPX_SWEEP_FUSED=0, read per chunk) — the two paths sum in different orders, so they agree to the
 same 1e-9 tolerance, and their argmax agrees exactly or at a reported tie."""
 import os
@@ -38,6 +38,10 @@ CASES = [
     (255, 8, "matern52", 999, "ucb"),
     (256, 4, "rbf", 20000, "logei"),
     (256, 16, "rbf", 1500, "ei"),
+    (257, 8, "rbf", 3001, "logei"),
+    (300, 4, "matern52", 2500, "ei"),
+    (384, 8, "scale_linear_matern52", 1800, "logei"),
+    (384, 13, "rbf", 700, "ucb"),
 ]
 
 
