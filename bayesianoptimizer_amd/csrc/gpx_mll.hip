@@ -53,7 +53,10 @@ __global__ void __launch_bounds__(WG) mll_grad_kernel(gpx_kernel_params p, int n
   // K^{-1}, so the per-unit contractions add up to the contraction of the full tile; alpha alpha^T enters in
   // chunk 0 only.  Without the split the few deepest tiles (I = 0: k over all of npad) set the critical path.
   const int kbeg = i0 + (int)blockIdx.y * kc;
-  double* dst = part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * GPX_MLL_NOUT;
+  // gridDim.z = 8 (tiny grids, npad <= 256): workgroup z contracts only slab z of the tile (the MFMA product is
+  // recomputed per slab, ~2 us); one workgroup over all eight slabs took 44 us at n = 128
+  double* dst = part + (((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * GPX_MLL_NOUT;
+  const bool all_slabs = gridDim.z == 1;
   if (kbeg >= npad) {
     for (int o = threadIdx.x; o < GPX_MLL_NOUT; o += WG) dst[o] = 0.0;
     return;
@@ -101,6 +104,7 @@ __global__ void __launch_bounds__(WG) mll_grad_kernel(gpx_kernel_params p, int n
   // 256 threads contract the slab element by element (a rolled loop keeps register pressure flat).
 #pragma unroll
   for (int sl = 0; sl < MT / SW; ++sl) {
+    if (!all_slabs && sl != (int)blockIdx.z) continue;  // uniform per workgroup
     if ((w & 1) == (sl >> 2)) {
 #pragma unroll
       for (int a = 0; a < Tile::WM; ++a)
@@ -262,11 +266,14 @@ int mll_kchunk(int64_t npad) {
   return (int)(kc < 512 ? 512 : kc);
 }
 
+// epilogue slabs split over workgroups (gridDim.z) for the tiny grids of npad <= 256
+static int mll_slab_split(int64_t npad) { return npad <= 256 ? MT / 16 : 1; }
+
 size_t mll_workspace_bytes(int64_t npad) {
   const int64_t T = npad / MT;
   const int64_t kc = mll_kchunk(npad);
   const int64_t ny = (npad + kc - 1) / kc;
-  return ((size_t)(T * (T + 1) / 2) * ny + 256 + 1) * GPX_MLL_NOUT * sizeof(double);
+  return ((size_t)(T * (T + 1) / 2) * ny * mll_slab_split(npad) + 256 + 1) * GPX_MLL_NOUT * sizeof(double);
 }
 
 hipError_t launch_mll(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
@@ -276,7 +283,7 @@ hipError_t launch_mll(Context* c, const gpx_kernel_params& p, int n, int npad, c
   const int T = npad / MT;
   const int tiles = T * (T + 1) / 2;
   const int kc = mll_kchunk(npad);
-  const dim3 grid(tiles, (npad + kc - 1) / kc);
+  const dim3 grid(tiles, (npad + kc - 1) / kc, mll_slab_split(npad));
 #define GPX_MLL_K(D, K) mll_grad_kernel<D, K><<<grid, WG, 0, c->stream>>>(p, n, npad, X, ldx, W, ldw, alpha, nrhs, kc, part)
 #define GPX_MLL(D)                                                         \
   (p.kind == GPX_KERNEL_RBF        ? GPX_MLL_K(D, GPX_KERNEL_RBF)          \
@@ -292,7 +299,7 @@ hipError_t launch_mll(Context* c, const gpx_kernel_params& p, int n, int npad, c
     GPX_MLL(32);
 #undef GPX_MLL
 #undef GPX_MLL_K
-  const int64_t rows = (int64_t)tiles * grid.y;
+  const int64_t rows = (int64_t)tiles * grid.y * grid.z;
   const int64_t rpb = std::max<int64_t>(64, (rows + 255) / 256);
   const int nb = (int)((rows + rpb - 1) / rpb);
   double* stage = part + rows * GPX_MLL_NOUT;  // nb <= 256 rows
