@@ -216,25 +216,28 @@ __global__ void __launch_bounds__(WG) trmm_sumsq_kernel(const double* __restrict
   }
 }
 
-// ---- 1+2 fused, small n (npad <= 256, one output) ----------------------------------------------------------
+// ---- 1+2 fused, small n (npad <= 256) ----------------------------------------------------------
 // At small n the K* round trip through HBM and the 128-row trmm tiles (whose triangle is at most two tiles deep)
 // cost more than the product (profiles/r01_small_n_rates.log, n = 256: kstar 2.2 + trmm 6.4 ms per 2^22 candidates
 // at 43 TF/s).  Here one wave owns 16 candidates and walks k in steps of 4: each lane evaluates K*[k][c]
 // (k = k0 + lane/16, c = lane%16) straight into the B operand of v_mfma_f64_16x16x4 (no K* buffer), and the A
 // operands W[k][16 ib + lane%16] of the row blocks ib >= k/16 come from L2 (W is npad^2 fp64 <= 512 KiB, shared by
 // every workgroup).  The triangle is walked in 16-row blocks, so the diagonal waste is 1/16 instead of 1/2 of a
-// 128-row tile.  Outputs per candidate: mu (alpha^T K*, no constant mean) and ss = |W^T K*|^2, in the layout of one
-// mu_part / ss_part block so finalize_kernel runs unchanged with nJB = nI = 1.  The summation order differs from the
+// 128-row tile.  Outputs per candidate: mu (alpha^T K* per output, no constant mean) and ss = |W^T K*|^2, in the
+// layout of one mu_part / ss_part block so finalize_kernel runs unchanged with nJB = nI = 1.  The summation order differs from the
 // unfused path (both are checked against the oracle at the same tolerance).
-template <int NPAD, int DMAX, int KIND>
+// NR = 1 (acquisition, single-output posterior) or GPX_MAX_RHS (multi-output posterior, alpha zero-padded to 8 columns
+// so the mean loop has no nrhs test; mu_out[q][c] for q < nrhs).
+template <int NPAD, int DMAX, int KIND, int NR>
 __global__ void __launch_bounds__(WG) sweep_small_kernel(gpx_kernel_params p, int n, const double* __restrict__ X,
-                                                         int64_t ldx, const double* __restrict__ alpha,
+                                                         int64_t ldx, const double* __restrict__ alpha, int nrhs,
                                                          const double* __restrict__ W, int64_t ldw,
                                                          const double* __restrict__ Xs, int64_t ldxs, int64_t m_chunk,
-                                                         double* __restrict__ mu_out, double* __restrict__ ss_out) {
+                                                         int64_t C, double* __restrict__ mu_out,
+                                                         double* __restrict__ ss_out) {
   constexpr int NRB = NPAD / 16;
   constexpr bool LIN = KIND == GPX_KERNEL_SCALE_LINEAR_MATERN52;
-  __shared__ double sx[NPAD][DMAX], sr[LIN ? NPAD : 1][DMAX], sa[NPAD];
+  __shared__ double sx[NPAD][DMAX], sr[LIN ? NPAD : 1][DMAX], sa[NPAD][NR];
   const int d = p.d;
   for (int e = threadIdx.x; e < NPAD * DMAX; e += WG) {
     const int r = e / DMAX, k = e % DMAX;
@@ -242,7 +245,10 @@ __global__ void __launch_bounds__(WG) sweep_small_kernel(gpx_kernel_params p, in
     sx[r][k] = (k < d) ? v / p.lengthscale[k] : 0.0;
     if (LIN) sr[r][k] = (k < d) ? v * p.linear_variance[k] : 0.0;
   }
-  for (int r = threadIdx.x; r < NPAD; r += WG) sa[r] = r < n ? alpha[r] : 0.0;
+  for (int e = threadIdx.x; e < NPAD * NR; e += WG) {
+    const int r = e / NR, q = e % NR;
+    sa[r][q] = (r < n && q < nrhs) ? alpha[(int64_t)r * nrhs + q] : 0.0;
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int kr = lane >> 4;
@@ -253,7 +259,9 @@ __global__ void __launch_bounds__(WG) sweep_small_kernel(gpx_kernel_params p, in
   d4 acc[NRB];
 #pragma unroll
   for (int ib = 0; ib < NRB; ++ib) acc[ib] = (d4){0.0, 0.0, 0.0, 0.0};
-  double mu = 0.0;
+  double mu[NR];
+#pragma unroll
+  for (int q = 0; q < NR; ++q) mu[q] = 0.0;
   const double* __restrict__ Wl = W + (int64_t)kr * ldw + (lane & 15);
 #pragma unroll
   for (int kb = 0; kb < NRB; ++kb) {
@@ -274,7 +282,8 @@ __global__ void __launch_bounds__(WG) sweep_small_kernel(gpx_kernel_params p, in
       }
       double kv = cov_from_r2(KIND, p.outputscale, r2, lv);
       kv = j < n ? kv : 0.0;
-      mu += sa[j] * kv;
+#pragma unroll
+      for (int q = 0; q < NR; ++q) mu[q] += sa[j][q] * kv;
 #pragma unroll
       for (int ib = kb; ib < NRB; ++ib) acc[ib] = mfma16x16x4(Wl[(int64_t)k0 * ldw + 16 * ib], kv, acc[ib]);
     }
@@ -286,10 +295,15 @@ __global__ void __launch_bounds__(WG) sweep_small_kernel(gpx_kernel_params p, in
     for (int r = 0; r < 4; ++r) s += acc[ib][r] * acc[ib][r];
   s += __shfl_xor(s, 16);
   s += __shfl_xor(s, 32);
-  mu += __shfl_xor(mu, 16);
-  mu += __shfl_xor(mu, 32);
+#pragma unroll
+  for (int q = 0; q < NR; ++q) {
+    mu[q] += __shfl_xor(mu[q], 16);
+    mu[q] += __shfl_xor(mu[q], 32);
+  }
   if (lane < 16 && valid) {
-    mu_out[c] = mu;
+#pragma unroll
+    for (int q = 0; q < NR; ++q)
+      if (q < nrhs) mu_out[(int64_t)q * C + c] = mu[q];
     ss_out[c] = s;
   }
 }
@@ -439,14 +453,14 @@ size_t sweep_workspace_bytes(int64_t npad, int64_t nrhs, int64_t m) {
   return b + 256;
 }
 
-// The fused small-n sweep covers npad <= 256, one output, d <= 16 and the fp64 covariance build; the rest takes the
-// K* + trmm path.  An npad = 384 instance (d <= 8, 226 VGPRs, 2 waves/SIMD) measured slower than the K* + trmm path
+// The fused small-n sweep covers npad <= 256, d <= 16 (1..8 outputs) and the fp64 covariance build; the rest takes
+// the K* + trmm path.  An npad = 384 instance (d <= 8, 226 VGPRs, 2 waves/SIMD) measured slower than the K* + trmm path
 // (2.20e8 vs 2.66e8 candidates/s at n = 384, profiles/r01_small_n_rates.log): 24 row blocks of A operands per k-step
 // from L2 and half the occupancy of the npad = 256 instance.  GPX_SWEEP_FUSED=0 forces the unfused path (A/B
 // measurements, parity tests of both paths).
 bool sweep_fused_ok(const gpx_kernel_params& p, int npad, int nrhs) {
   const char* e = getenv("GPX_SWEEP_FUSED");  // read per chunk: tests flip it inside one process
-  return !(e && e[0] == '0') && (npad == 128 || npad == 256) && nrhs == 1 && p.d <= 16 && !p.cov_fp32;
+  return !(e && e[0] == '0') && (npad == 128 || npad == 256) && p.d <= 16 && !p.cov_fp32;
 }
 
 hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
@@ -462,8 +476,10 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
     LaunchTimer tm(c, GPX_TIMER_TRMM);
     const int nwg = (int)((m_chunk + 63) / 64);
 #define GPX_SMALL_K(NP, D, K)                                                                                       \
-  sweep_small_kernel<NP, D, K><<<nwg, WG, 0, c->stream>>>(p, n, X, ldx, alpha, W, ldw, Xs, ldxs, m_chunk, b.mu_part, \
-                                                          b.ss_part)
+  (nrhs == 1 ? sweep_small_kernel<NP, D, K, 1><<<nwg, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, W, ldw, Xs, ldxs,  \
+                                                                           m_chunk, C, b.mu_part, b.ss_part)          \
+             : sweep_small_kernel<NP, D, K, GPX_MAX_RHS><<<nwg, WG, 0, c->stream>>>(                                  \
+                   p, n, X, ldx, alpha, nrhs, W, ldw, Xs, ldxs, m_chunk, C, b.mu_part, b.ss_part))
 #define GPX_SMALL_D(NP, D)                                                                                          \
   (p.kind == GPX_KERNEL_RBF        ? GPX_SMALL_K(NP, D, GPX_KERNEL_RBF)                                             \
    : p.kind == GPX_KERNEL_MATERN52 ? GPX_SMALL_K(NP, D, GPX_KERNEL_MATERN52)                                        \

@@ -1,4 +1,4 @@
-"""Fused small-n sweep (sweep_small_kernel: npad <= 256, one output, d <= 16, fp64 covariance build; n = 257..384
+"""Fused small-n sweep (sweep_small_kernel: npad <= 256, d <= 16, 1..8 outputs, fp64 covariance build; n = 257..384
 cases check the boundary, where both sides take the K* + trmm path): every case is checked against the oracle at the parity tolerances of tests/test_gpu_parity.py, and against the unfused K* + trmm path
 of the same library (GPX_SWEEP_FUSED=0, read per chunk) — the two paths sum in different orders, so they agree to the
 same 1e-9 tolerance, and their argmax agrees exactly or at a reported tie."""
@@ -78,3 +78,26 @@ def test_fused_sweep_nan_candidates_never_win(engine):
     ok = ~np.isnan(Xs).any(axis=1)
     np.testing.assert_allclose(sg_f[ok], sg_u[ok], rtol=1e-9, atol=1e-12)
     assert bi_f == bi_u
+
+
+@pytest.mark.parametrize("n,d,nrhs,kind", [(60, 5, 8, "rbf"), (200, 8, 3, "matern52"), (256, 16, 2, "scale_linear_matern52")])
+def test_fused_multi_output_posterior(engine, n, d, nrhs, kind):
+    """Multi-output posterior (Bayesian2.predict's 8 outputs sharing X): per-output means from the fused kernel."""
+    X, y = O.synthetic_problem(n, d, n + nrhs)
+    Y = np.stack([y * (r + 1) - 0.3 * r for r in range(nrhs)], axis=1)
+    kp, op = pair(kind, d, noise=1e-4, const_mean=0.2)
+    ost = O.fit(X, Y, op)
+    st = engine.fit(t(X), t(Y), kp)
+    Xs = O.sobol_candidates(3000, d, n)
+    out = {}
+    for fused in (True, False):
+        os.environ["GPX_SWEEP_FUSED"] = "1" if fused else "0"
+        try:
+            mu, var = engine.posterior(st, t(Xs))
+        finally:
+            os.environ.pop("GPX_SWEEP_FUSED", None)
+        out[fused] = (mu.cpu().numpy(), var.cpu().numpy())
+    mu_r, var_r = O.posterior(ost, Xs)
+    kdiag = O.kernel_diag(Xs, op)
+    check_posterior(out[True][0], out[True][1], mu_r.reshape(3000, nrhs), var_r, kdiag)
+    check_posterior(out[True][0], out[True][1], out[False][0], out[False][1], kdiag)
