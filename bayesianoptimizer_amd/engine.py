@@ -507,16 +507,18 @@ class GPEngine:
         (T outputs sharing the hyperparameters).  Synchronises."""
         X = self._as_f64(X, "X")
         y = self._as_f64(y, "y")
-        err = None
+        # The gradient is queued right behind the fit and the pivot-failure word is read after both (one host round
+        # trip per evaluation instead of two; a gradient computed on a failed factor is discarded).
+        piv = -1
         for jit in jitters:
-            try:
-                state = self.fit(X, y, params.replace(jitter=params.jitter + jit), out=state)
+            state = self.fit(X, y, params.replace(jitter=params.jitter + jit), check=False, out=state)
+            out = self.mll_grad(state, y)
+            v = out.cpu().numpy()
+            piv = state.pivot_failure()
+            if piv < 0:
                 break
-            except NotPositiveDefiniteError as e:
-                err = e
         else:
-            raise err
-        v = self.mll_grad(state, y).cpu().numpy()
+            raise NotPositiveDefiniteError(piv)
         d = X.shape[1]
         res = {
             "nll": float(v[_capi.MLL_NLL]), "quad": float(v[_capi.MLL_QUAD]), "logdet": float(v[_capi.MLL_LOGDET]),
