@@ -80,10 +80,8 @@ class KernelParams:
         c = KernelParamsC()
         c.kind = self.kind_id
         c.d = d
-        for k, v in enumerate(self.lengthscales(d)):
-            c.lengthscale[k] = v
-        for k, v in enumerate(self.linear_variances(d)):
-            c.linear_variance[k] = v
+        c.lengthscale[:d] = self.lengthscales(d)  # slice assignment: one ctypes call per array (to_c runs per fit)
+        c.linear_variance[:d] = self.linear_variances(d)
         c.outputscale = float(self.outputscale)
         c.noise = float(self.noise)
         c.jitter = float(self.jitter)
