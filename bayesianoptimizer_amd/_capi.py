@@ -88,6 +88,8 @@ _PROTOS = {
     "gpx_set_stream": (c_int32, [_h, c_void_p]),
     "gpx_last_error": (c_char_p, [_h]),
     "gpx_padded_n": (c_int64, [c_int64]),
+    "gpx_kernel_params_size": (c_size_t, []),
+    "gpx_acq_params_size": (c_size_t, []),
     "gpx_gram_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64]),
     "gpx_potrf_f64": (c_int32, [_h, c_int64, _p, c_int64, _p, _p]),
     "gpx_trtri_workspace_size": (c_int32, [c_int64, POINTER(c_size_t)]),
@@ -160,6 +162,11 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    # the struct definitions above must match the ones compiled into the library (a truncated struct would make the
+    # library read past the caller's object, include/gpx.h)
+    for cls, fn in ((KernelParamsC, lib.gpx_kernel_params_size), (AcqParamsC, lib.gpx_acq_params_size)):
+        if ctypes.sizeof(cls) != fn():
+            raise GPXLibraryError(f"{cls.__name__} is {ctypes.sizeof(cls)} bytes, libgpx expects {fn()}")
     _lib = lib
     return lib
 

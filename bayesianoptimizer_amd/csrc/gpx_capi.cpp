@@ -24,13 +24,6 @@ gpx_status hip_check(Context* c, hipError_t e, const char* where) {
   return fail(c, GPX_HIP_ERROR, std::string(where) + ": " + hipGetErrorString(e));
 }
 
-gpx_status use_device(Context* c) {
-  int cur = -1;
-  hipError_t e = hipGetDevice(&cur);
-  if (e != hipSuccess) return hip_check(c, e, "hipGetDevice");
-  if (cur != c->device) return hip_check(c, hipSetDevice(c->device), "hipSetDevice");
-  return GPX_OK;
-}
 
 int64_t padded(int64_t n) { return ((n + GPX_TILE - 1) / GPX_TILE) * GPX_TILE; }
 
@@ -45,6 +38,14 @@ gpx_status check_params(Context* c, const gpx_kernel_params* p) {
       return fail(c, GPX_INVALID_ARG, "lengthscale[" + std::to_string(k) + "] must be positive and finite");
   if (!(p->outputscale >= 0.0) || !(p->noise >= 0.0) || !(p->jitter >= 0.0))
     return fail(c, GPX_INVALID_ARG, "outputscale/noise/jitter must be non-negative");
+  // The trailing int32 pair is part of the contract: a caller whose struct definition stops before it (552 instead of
+  // gpx_kernel_params_size() bytes) would hand over whatever follows its struct in memory, and a stray non-zero
+  // cov_fp32 would silently switch the covariance build to fp32.  Anything but {0, 1} / 0 is rejected.
+  if (p->cov_fp32 != 0 && p->cov_fp32 != 1)
+    return fail(c, GPX_INVALID_ARG, "cov_fp32 must be 0 or 1 (got " + std::to_string(p->cov_fp32) +
+                                        "; is the caller's gpx_kernel_params " + std::to_string(sizeof(gpx_kernel_params)) +
+                                        " bytes?)");
+  if (p->reserved != 0) return fail(c, GPX_INVALID_ARG, "gpx_kernel_params.reserved must be 0");
   return GPX_OK;
 }
 
@@ -64,6 +65,11 @@ gpx_status check_ld(Context* c, int64_t ld, int64_t minimum, const char* name, b
     gpx_status _st = (expr);        \
     if (_st != GPX_OK) return _st;  \
   } while (0)
+
+// Makes the handle's device current for the rest of the calling entry point and restores the caller's device on return.
+#define GPX_USE_DEVICE(c)                                  \
+  gpx::DeviceScope _gpx_dev((c)->device);                  \
+  if (_gpx_dev.err != hipSuccess) return hip_check((c), _gpx_dev.err, "hipSetDevice")
 
 #define GPX_NONNULL(c, ptr) \
   do { if (!(ptr)) return fail((c), GPX_INVALID_ARG, #ptr " is NULL"); } while (0)
@@ -112,6 +118,10 @@ const char* gpx_version(void) { return kVersion; }
 
 int64_t gpx_padded_n(int64_t n) { return padded(n); }
 
+size_t gpx_kernel_params_size(void) { return sizeof(gpx_kernel_params); }
+
+size_t gpx_acq_params_size(void) { return sizeof(gpx_acq_params); }
+
 gpx_status gpx_create(int32_t device, gpx_handle* out) {
   if (!out) return GPX_INVALID_ARG;
   *out = nullptr;
@@ -121,9 +131,12 @@ gpx_status gpx_create(int32_t device, gpx_handle* out) {
   Context* c = new (std::nothrow) Context();
   if (!c) return GPX_HIP_ERROR;
   c->device = device;
-  if (use_device(c) != GPX_OK) {
-    delete c;
-    return GPX_HIP_ERROR;
+  {
+    gpx::DeviceScope dev(device);  // the device must be selectable; the caller's current device is left as it was
+    if (dev.err != hipSuccess) {
+      delete c;
+      return GPX_HIP_ERROR;
+    }
   }
   *out = reinterpret_cast<gpx_handle>(c);
   return GPX_OK;
@@ -167,7 +180,7 @@ static gpx_status gram_impl(gpx_handle h, const gpx_kernel_params* p, int64_t n,
   const int64_t npad = padded(n);
   GPX_TRY(check_ld(c, ldx, p->d, "X", false));
   GPX_TRY(check_ld(c, ldk, npad, "K", true));
-  GPX_TRY(use_device(c));
+  GPX_USE_DEVICE(c);
   return hip_check(c, gpx::launch_gram(c, *p, (int)n, (int)npad, X, ldx, K, ldk, gpx::Batch(), 0, info), "gram");
 }
 
@@ -186,7 +199,7 @@ static gpx_status potrf_impl(gpx_handle h, int64_t n, double* A, int64_t lda, do
   GPX_NONNULL(c, info);
   const int64_t npad = padded(n);
   GPX_TRY(check_ld(c, lda, npad, "A", true));
-  GPX_TRY(use_device(c));
+  GPX_USE_DEVICE(c);
   if (clear_info) GPX_TRY(hip_check(c, hipMemsetAsync(info, 0, sizeof(int32_t), c->stream), "memset info"));
   return hip_check(c, gpx::launch_potrf(c, (int)npad, A, lda, Dinv, info, gpx::Batch(), W, ldw), "potrf");
 }
@@ -214,7 +227,7 @@ static gpx_status trtri_impl(gpx_handle h, int64_t n, const double* L, int64_t l
   GPX_TRY(check_ld(c, ldl, npad, "L", true));
   GPX_TRY(check_ld(c, ldw, npad, "W", true));
   if (ws_bytes < trtri_ws(npad)) return fail(c, GPX_INVALID_ARG, "trtri workspace too small");
-  GPX_TRY(use_device(c));
+  GPX_USE_DEVICE(c);
   return hip_check(c, gpx::launch_trtri(c, (int)npad, L, ldl, Dinv, W, ldw, align256(ws), gpx::Batch(), diag_done),
                    "trtri");
 }
@@ -244,7 +257,7 @@ gpx_status gpx_alpha_f64(gpx_handle h, int64_t n, const double* W, int64_t ldw, 
   GPX_TRY(check_ld(c, ldw, npad, "W", true));
   GPX_TRY(check_ld(c, ldy, nrhs, "Y", false));
   if (ws_bytes < alpha_ws(npad, nrhs)) return fail(c, GPX_INVALID_ARG, "alpha workspace too small");
-  GPX_TRY(use_device(c));
+  GPX_USE_DEVICE(c);
   double* zpart = align256(ws);
   double* z = zpart + (size_t)(npad / 128) * npad * nrhs;
   return hip_check(c, gpx::launch_alpha(c, (int)n, (int)npad, W, ldw, Y, ldy, (int)nrhs, const_mean, alpha, zpart, z),
@@ -327,7 +340,7 @@ gpx_status gpx_append_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n_ol
   size_t need = 0;
   GPX_TRY(gpx_append_workspace_size(n_old, n_new, nrhs, &need));
   if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "append workspace too small");
-  GPX_TRY(use_device(c));
+  GPX_USE_DEVICE(c);
   double* base = align256(ws);
   GPX_TRY(hip_check(c, hipMemsetAsync(info, 0, sizeof(int32_t), c->stream), "memset info"));
   GPX_TRY(hip_check(c, gpx::launch_append(c, *p, (int)n_old, (int)n_new, X, ldx, L, ldl, Dinv, W, ldw, info, base),
@@ -385,7 +398,7 @@ gpx_status gpx_fit_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t
   size_t need = 0;
   GPX_TRY(gpx_fit_batched_workspace_size(n, nrhs, batch, &need));
   if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "batched fit workspace too small");
-  GPX_TRY(use_device(c));
+  GPX_USE_DEVICE(c);
   gpx::Batch bt;
   bt.count = (int)batch;
   bt.x = stride_x;
@@ -435,7 +448,7 @@ gpx_status gpx_mll_grad_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n,
   if (nrhs < 1 || nrhs > GPX_MAX_RHS) return fail(c, GPX_INVALID_ARG, "nrhs must be in [1, 8]");
   GPX_TRY(check_ld(c, ldy, nrhs, "Y", false));
   if (ws_bytes < gpx::mll_workspace_bytes(npad) + 256) return fail(c, GPX_INVALID_ARG, "mll workspace too small");
-  GPX_TRY(use_device(c));
+  GPX_USE_DEVICE(c);
   return hip_check(c, gpx::launch_mll(c, *p, (int)n, (int)npad, X, ldx, Y, ldy, (int)nrhs, L, ldl, W, ldw, alpha, out,
                                       align256(ws)), "mll");
 }
@@ -472,7 +485,7 @@ gpx_status gpx_moments_grad_f64(gpx_handle h, const gpx_kernel_params* p, int64_
   size_t need = 0;
   GPX_TRY(gpx_moments_grad_workspace_size(n, m, &need));
   if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "moments_grad workspace too small");
-  GPX_TRY(use_device(c));
+  GPX_USE_DEVICE(c);
   return hip_check(c, gpx::launch_moments_grad(c, *p, (int)n, (int)npad, X, ldx, W, ldw, alpha, Xs, ldxs, (int)m,
                                                (int)q, mean, dmean, cov, dcov, align256(ws)),
                    "moments_grad");
@@ -523,7 +536,7 @@ gpx_status gpx_posterior_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n
   GPX_TRY(check_ld(c, ldmean, nrhs, "mean", false));
   gpx::SweepBuffers b;
   GPX_TRY(carve_sweep(c, npad, nrhs, m, ws, ws_bytes, &b));
-  GPX_TRY(use_device(c));
+  GPX_USE_DEVICE(c);
   for (int64_t s = 0; s < m; s += b.chunk) {
     const int64_t mc = (m - s) < b.chunk ? (m - s) : b.chunk;
     GPX_TRY(hip_check(c,
@@ -546,6 +559,7 @@ gpx_status gpx_acquire_argmax_f64(gpx_handle h, const gpx_kernel_params* p, int6
   if (m < 1) return fail(c, GPX_INVALID_ARG, "m must be >= 1");
   if (!a) return fail(c, GPX_INVALID_ARG, "acquisition params pointer is NULL");
   if (a->kind < GPX_ACQ_EI || a->kind > GPX_ACQ_VARIANCE) return fail(c, GPX_INVALID_ARG, "unknown acquisition kind");
+  if (a->reserved != 0) return fail(c, GPX_INVALID_ARG, "gpx_acq_params.reserved must be 0");
   if (!(a->y_scale > 0.0)) return fail(c, GPX_INVALID_ARG, "y_scale must be positive");
   if (a->kind == GPX_ACQ_UCB && !(a->beta >= 0.0)) return fail(c, GPX_INVALID_ARG, "UCB beta must be >= 0");
   if (index_offset < 0) return fail(c, GPX_INVALID_ARG, "index_offset must be >= 0");
@@ -561,7 +575,7 @@ gpx_status gpx_acquire_argmax_f64(gpx_handle h, const gpx_kernel_params* p, int6
   GPX_TRY(check_ld(c, ldxs, p->d, "Xs", false));
   gpx::SweepBuffers b;
   GPX_TRY(carve_sweep(c, npad, 1, m, ws, ws_bytes, &b));
-  GPX_TRY(use_device(c));
+  GPX_USE_DEVICE(c);
   int64_t rec = 0;
   for (int64_t s = 0; s < m; s += b.chunk) {
     const int64_t mc = (m - s) < b.chunk ? (m - s) : b.chunk;
@@ -584,7 +598,7 @@ gpx_status gpx_argmax_combine_f64(gpx_handle h, const double* vals, const int64_
   GPX_NONNULL(c, idx);
   GPX_NONNULL(c, best_val);
   GPX_NONNULL(c, best_idx);
-  GPX_TRY(use_device(c));
+  GPX_USE_DEVICE(c);
   return hip_check(c, gpx::launch_argmax_final(c, vals, idx, count, best_val, best_idx), "argmax_combine");
 }
 
@@ -649,7 +663,7 @@ gpx_status gpx_svgp_prepare_f64(gpx_handle h, const gpx_kernel_params* p, int64_
   size_t need = 0;
   GPX_TRY(gpx_svgp_prepare_workspace_size(M, ntask, &need));
   if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "svgp prepare workspace too small");
-  GPX_TRY(use_device(c));
+  GPX_USE_DEVICE(c);
   const SvgpPrepLayout lay = svgp_prep_layout(Mpad);
   char* base = reinterpret_cast<char*>(align256(ws));
   auto at = [&](int64_t t, size_t off) { return reinterpret_cast<double*>(base + lay.total * t + off); };
@@ -722,7 +736,7 @@ gpx_status gpx_svgp_predict_f64(gpx_handle h, const gpx_kernel_params* p, int64_
   gpx::SweepBuffers b;
   GPX_TRY(carve_sweep(c, Mpad, 1, m, ws, ws_bytes, &b));
   double* ss2 = reinterpret_cast<double*>(((uintptr_t)(b.rec_idx + (m + 255) / 256 + 1) + 255) & ~(uintptr_t)255);
-  GPX_TRY(use_device(c));
+  GPX_USE_DEVICE(c);
   for (int64_t s = 0; s < m; s += b.chunk) {
     const int64_t mc = (m - s) < b.chunk ? (m - s) : b.chunk;
     for (int64_t t = 0; t < ntask; ++t) {
@@ -754,7 +768,7 @@ gpx_status gpx_topk_f64(gpx_handle h, const double* scores, int64_t m, int64_t k
   if (m < 1 || m > ((int64_t)1 << 30)) return fail(c, GPX_INVALID_ARG, "m must be in [1, 2^30]");
   if (k < 1 || k > m) return fail(c, GPX_INVALID_ARG, "k must be in [1, m]");
   if (ws_bytes < gpx::topk_workspace_bytes(m)) return fail(c, GPX_INVALID_ARG, "topk workspace too small");
-  GPX_TRY(use_device(c));
+  GPX_USE_DEVICE(c);
   return hip_check(c, gpx::launch_topk(c, scores, m, k, idx_out, val_out, ws, ws_bytes), "topk");
 }
 
@@ -769,7 +783,7 @@ gpx_status gpx_fps_f64(gpx_handle h, const double* X, int64_t m, int64_t d, int6
   if (k < 1 || k > m) return fail(c, GPX_INVALID_ARG, "k must be in [1, m]");
   if (start < 0 || start >= m) return fail(c, GPX_INVALID_ARG, "start index outside [0, m)");
   GPX_TRY(check_ld(c, ldx, d, "X", false));
-  GPX_TRY(use_device(c));
+  GPX_USE_DEVICE(c);
   return hip_check(c, gpx::launch_fps(c, X, m, (int)d, ldx, k, start, idx_out), "fps");
 }
 

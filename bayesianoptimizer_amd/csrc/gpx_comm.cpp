@@ -36,7 +36,8 @@ gpx_status gpx_comm_init(gpx_handle h, const uint8_t* id, int32_t nranks, int32_
   gpx::Context* c = reinterpret_cast<gpx::Context*>(h);
   if (!c || !id || !out || nranks < 1 || rank < 0 || rank >= nranks) return GPX_INVALID_ARG;
   *out = nullptr;
-  if (hipSetDevice(c->device) != hipSuccess) return GPX_HIP_ERROR;
+  gpx::DeviceScope dev(c->device);  // RCCL binds the communicator to the current device
+  if (dev.err != hipSuccess) return GPX_HIP_ERROR;
   ncclUniqueId uid;
   memcpy(&uid, id, sizeof(uid));
   gpx_comm cm = new gpx_comm_s();
@@ -58,9 +59,12 @@ gpx_status gpx_comm_destroy(gpx_comm cm) {
   return r == ncclSuccess ? GPX_OK : GPX_RCCL_ERROR;
 }
 
+// workspace: the 16-byte send record, then the nranks gathered records (256-aligned)
+static size_t exchange_ws_bytes(int nranks) { return 256 + 256 + (size_t)nranks * 16; }
+
 gpx_status gpx_allreduce_argmax_workspace_size(gpx_comm cm, size_t* bytes) {
   if (!cm || !bytes) return GPX_INVALID_ARG;
-  *bytes = (size_t)cm->nranks * 16 + 256;
+  *bytes = exchange_ws_bytes(cm->nranks);
   return GPX_OK;
 }
 
@@ -72,20 +76,27 @@ gpx_status gpx_allreduce_argmax(gpx_handle h, gpx_comm cm, double* best_val, int
     c->last_error = "best_val / best_idx / ws is NULL";
     return GPX_INVALID_ARG;
   }
-  if (ws_bytes < (size_t)cm->nranks * 16 + 256) {
+  if (ws_bytes < exchange_ws_bytes(cm->nranks)) {
     c->last_error = "allreduce_argmax workspace too small";
     return GPX_INVALID_ARG;
   }
+  gpx::DeviceScope dev(c->device);
+  if (dev.err != hipSuccess) {
+    c->last_error = "hipSetDevice failed";
+    return GPX_HIP_ERROR;
+  }
+  // one record {fp64 value, int64 index} per rank, ONE all-gather of 16 bytes each, then the deterministic combine
   uintptr_t u = (reinterpret_cast<uintptr_t>(ws) + 255) & ~(uintptr_t)255;
-  double* vals = reinterpret_cast<double*>(u);
-  int64_t* idx = reinterpret_cast<int64_t*>(vals + cm->nranks);
-  ncclResult_t r = ncclGroupStart();
-  if (r == ncclSuccess) r = ncclAllGather(best_val, vals, 1, ncclFloat64, cm->comm, c->stream);
-  if (r == ncclSuccess) r = ncclAllGather(best_idx, idx, 1, ncclInt64, cm->comm, c->stream);
-  const ncclResult_t r2 = ncclGroupEnd();
+  int64_t* send = reinterpret_cast<int64_t*>(u);
+  int64_t* recv = send + 32;  // 256 bytes further
+  hipError_t e = gpx::launch_record_pack(c, best_val, best_idx, send);
+  if (e != hipSuccess) {
+    c->last_error = std::string("record_pack: ") + hipGetErrorString(e);
+    return GPX_HIP_ERROR;
+  }
+  const ncclResult_t r = ncclAllGather(send, recv, 2, ncclInt64, cm->comm, c->stream);
   if (r != ncclSuccess) return rccl_fail(c, r, "ncclAllGather");
-  if (r2 != ncclSuccess) return rccl_fail(c, r2, "ncclGroupEnd");
-  const hipError_t e = gpx::launch_argmax_final(c, vals, idx, cm->nranks, best_val, best_idx);
+  e = gpx::launch_argmax_records(c, recv, cm->nranks, best_val, best_idx);
   if (e != hipSuccess) {
     c->last_error = std::string("argmax_combine: ") + hipGetErrorString(e);
     return GPX_HIP_ERROR;

@@ -32,6 +32,27 @@ struct Context {
   std::vector<hipEvent_t> free_events;
 };
 
+// Scoped device switch of one C ABI call: makes the handle's device current and restores the caller's current device
+// on exit, so a call on an engine of device k never moves the caller's (e.g. torch's) current device.
+struct DeviceScope {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceScope(int device) {
+    err = hipGetDevice(&prev);
+    if (err == hipSuccess && prev != device) {
+      err = hipSetDevice(device);
+      if (err != hipSuccess) prev = -1;
+    } else {
+      prev = -1;  // nothing to restore
+    }
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceScope(const DeviceScope&) = delete;
+  DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
 // Scoped timer: records a start event on construction and a stop event on destruction when the
 // timer's bit is set in the context's mask.
 struct LaunchTimer {
@@ -81,6 +102,10 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
                               int64_t rec_offset, int64_t index_offset);
 hipError_t launch_argmax_final(Context* c, const double* vals, const int64_t* idx, int64_t count, double* best_val,
                                int64_t* best_idx);
+// the cross-GPU exchange (gpx_comm.cpp): pack the device record into {double value; int64 index}, and reduce
+// `count` such packed records
+hipError_t launch_record_pack(Context* c, const double* best_val, const int64_t* best_idx, int64_t* rec);
+hipError_t launch_argmax_records(Context* c, const int64_t* rec, int64_t count, double* best_val, int64_t* best_idx);
 
 // SVGP predictive of one task over a chunk (gpx_sweep.hip); ss2: (Mpad/128) x C partials of the full W2 product.
 hipError_t launch_svgp_chunk(Context* c, const gpx_kernel_params& p, double min_var, int task, int M, int Mpad,

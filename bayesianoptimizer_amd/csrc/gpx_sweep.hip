@@ -383,16 +383,18 @@ __global__ void __launch_bounds__(WG) finalize_kernel(FinalizeArgs fa, int mode,
   }
 }
 
+// records e = 0 .. count-1 at vals[e * stride] / idx[e * stride] (stride 1: separate arrays; 2: packed 16-byte
+// (value, index) records of the cross-GPU exchange)
 __global__ void __launch_bounds__(WG) argmax_final_kernel(const double* __restrict__ vals,
                                                           const int64_t* __restrict__ idx, int64_t count,
-                                                          double* __restrict__ best_val,
+                                                          int stride, double* __restrict__ best_val,
                                                           int64_t* __restrict__ best_idx) {
   double bv = -INFINITY;
   int64_t bi = INT64_MAX;
   for (int64_t e = threadIdx.x; e < count; e += WG) {
-    double v = vals[e];
+    double v = vals[e * stride];
     if (v != v) v = -INFINITY;
-    argmax_merge(bv, bi, v, idx[e]);
+    argmax_merge(bv, bi, v, idx[e * stride]);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -626,7 +628,28 @@ hipError_t launch_svgp_chunk(Context* c, const gpx_kernel_params& p, double min_
 hipError_t launch_argmax_final(Context* c, const double* vals, const int64_t* idx, int64_t count, double* best_val,
                                int64_t* best_idx) {
   LaunchTimer tm(c, GPX_TIMER_ACQ);
-  argmax_final_kernel<<<1, WG, 0, c->stream>>>(vals, idx, count, best_val, best_idx);
+  argmax_final_kernel<<<1, WG, 0, c->stream>>>(vals, idx, count, 1, best_val, best_idx);
+  return hipGetLastError();
+}
+
+// (best_val, best_idx) -> one 16-byte record {double value; int64 index} (the send buffer of the exchange)
+__global__ void record_pack_kernel(const double* __restrict__ best_val, const int64_t* __restrict__ best_idx,
+                                   int64_t* __restrict__ rec) {
+  if (threadIdx.x == 0) {
+    rec[0] = __double_as_longlong(*best_val);
+    rec[1] = *best_idx;
+  }
+}
+
+hipError_t launch_record_pack(Context* c, const double* best_val, const int64_t* best_idx, int64_t* rec) {
+  record_pack_kernel<<<1, 64, 0, c->stream>>>(best_val, best_idx, rec);
+  return hipGetLastError();
+}
+
+hipError_t launch_argmax_records(Context* c, const int64_t* rec, int64_t count, double* best_val, int64_t* best_idx) {
+  LaunchTimer tm(c, GPX_TIMER_ACQ);
+  argmax_final_kernel<<<1, WG, 0, c->stream>>>(reinterpret_cast<const double*>(rec), rec + 1, count, 2, best_val,
+                                               best_idx);
   return hipGetLastError();
 }
 

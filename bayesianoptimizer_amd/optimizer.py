@@ -1,49 +1,60 @@
 """Drop-in ``BayesianOptimizer`` for ``scripts/run_optimization.py``.
 
-Constructor = the Bayesian7 superset signature (optimization/Bayesian7.py:202-218), so the reference driver
-(scripts/run_optimization.py:116-130) constructs it unchanged and calls ``optimize()`` which returns
-``(best_params[d] in physical units, best_value)`` (optimization/Bayesian7.py:729-733); the simulator duck type
-``configure_geometry / run_simulation / cleanup`` (simulation/taichi.py:33,46,145) is driven unchanged.
+The contract with the reference's caller is kept exactly; everything behind it is this package's own design:
 
-What differs, by design: the surrogate is an exact GP on the gpx engine (fp64, one shared factorisation for the
-8 outputs) instead of the batched SVGP; hyperparameters are fixed (MLL fitting: SURVEY §8f row 1).  Data flow,
-CSV resume, transforms, evaluation metrics, pool-scan acquisition (variance score -> top-K -> farthest-point
-sampling) and the objective/return contract follow Bayesian7.  ``acquisition="logei"|"ei"|"ucb"`` selects the
-analytic improvement sweep of optimization/Bayesian.py:96-113 over a Sobol grid instead, and
-``acquisition="qlogei"`` the reference's optimize_acqf on MC qLogEI (q = batch_size, L-BFGS-B restarts; acqf.py).
+* constructor — the Bayesian7 superset signature (``optimization/Bayesian7.py:202-218``), so
+  ``scripts/run_optimization.py:116-130`` builds it unchanged; ``optimize()`` returns ``(best_params[d] in physical
+  units, best_value)`` (``Bayesian7.py:729-733``); the simulator duck type ``configure_geometry / run_simulation /
+  cleanup`` (``simulation/taichi.py:33,46,145``) is driven unchanged;
+* persistence — the results CSV is the run's source of truth: same columns (``n,eta,sigma_y,width,height,x_01..``),
+  same ``%.8f`` rows, resume by reloading it (``Bayesian7.py:268-318``); metrics go to ``validation_log.csv``.
 
-Surface mapping (north star fit()/predict()/acquire()):
-  fit_gp_model()                 ≙ Bayesian7.fit_gp_model / Bayesian.fit_gp_model
-  predict(x_orig) -> (n, 8)      ≙ Bayesian2.predict (posterior mean in physical units)
-  acquire(k) -> Tensor[k, d]     ≙ Bayesian7 pool scan (:646-688) or Bayesian.optimize_acquisition_function
-  optimize_acquisition_function  ≙ Bayesian.py:96-113 (returns q unit-cube candidates)
+Behind it: the surrogate is an exact GP on the gpx engine (fp64, ONE factorisation shared by the 8 outputs) instead of
+the batched SVGP; its hyperparameters are fitted by exact marginal likelihood on the GPU each round (mll.py) or held
+fixed, in which case new observations are folded in by the bordered Cholesky (``ExactGP.append_observations``)
+instead of a refit.  Acquisition modes (``acquisition=``):
+
+* ``"variance"`` (default, Bayesian7's pool scan ``:646-688``): Latin-hypercube pool -> summed posterior variance on
+  the device -> top-K on the device (``gpx_topk_f64``, deterministic ties) -> farthest-point sampling on the device
+  (``gpx_fps_f64``) from a random start, as the reference's ``farthest_point_sampling`` (``:82-106``);
+* ``"logei" | "ei" | "ucb"`` (the analytic forms of ``optimization/Bayesian.py:96-113``'s qLogEI at q = 1): a
+  scrambled-Sobol grid scored on the device, best k by ``gpx_topk_f64``;
+* ``"qlogei"`` (``Bayesian.py:100-112``): ``optimize_acqf`` on MC qLogEI; batches larger than the engine's joint
+  q-batch limit (``GPX_MAX_Q``) are built greedily in chunks, each chunk conditioned on the ones before it with their
+  posterior means as fantasy observations (kriging believer).
+
+The scalar objective the improvement modes maximise is the one ``optimize()`` reports (``_scalar_objective``,
+``Bayesian7.py:597-609``): the weighted sum (``objective_weights``), one output (``objective_index``) or the sum of
+all outputs, negated in ``objective_mode="min"``.  The GP models log-standardised outputs (``Bayesian7.py:371-383``),
+so the acquisition scores that linear combination of the modelled outputs.
 """
 from __future__ import annotations
 
 import math
 import os
 from dataclasses import dataclass
-from typing import Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
 
+from . import _capi
 from .engine import GPEngine, KernelParams
 from .models import ExactGP
 from .transforms import LogInputStandardizer, LogOutputStandardizer
 
-OUTPUT_COLS = ["n", "eta", "sigma_y", "width", "height"]
+INPUT_COLUMNS = ("n", "eta", "sigma_y", "width", "height")  # simulator parameters, config/config.py order
 
 
 @dataclass
 class GPConfig:
-    """Knobs of optimization/Bayesian7.py:30-76 that still apply, plus the fixed exact-GP hyperparameters."""
+    """Knobs of ``optimization/Bayesian7.py:30-76`` that still apply, plus the exact-GP hyperparameters."""
 
     candidates_pool_size: int = 10000     # Bayesian7.py:57
     acq_batch_size: int = 500             # Bayesian7.py:60
-    acq_eval_batch_size: int = 2048       # kept for signature compatibility (the engine chunks internally)
+    acq_eval_batch_size: int = 2048       # accepted for signature compatibility (the engine chunks internally)
     K_BIG_CAP: int = 8000                 # Bayesian7.py:66
-    raw_samples: int = 1 << 14            # Sobol grid for the analytic improvement acquisitions
+    raw_samples: int = 1 << 14            # Sobol grid of the analytic improvement modes
     kernel: str = "scale_linear_matern52" # Bayesian6.py:471-473 / Bayesian7.py:162-166
     lengthscale: float = 1.0
     outputscale: float = 1.0
@@ -51,12 +62,14 @@ class GPConfig:
     noise: float = 1e-3
     jitter_val: float = 1e-4              # Bayesian6.py GPConfig.jitter_val; retried at 1e-2 (:487)
     beta: float = 4.0
-    # hyperparameters: learned each round like the reference's model fit (fit_gpytorch_mll, Bayesian.py:92-93;
-    # the driven variant trains them by ELBO, Bayesian7.py:451-538) — here by exact marginal likelihood on the
-    # GPU (mll.py), starting from the values above; False keeps them fixed
+    # exact marginal likelihood each round (fit_gpytorch_mll, Bayesian.py:92-93; the driven variant trains by ELBO,
+    # Bayesian7.py:451-538); False keeps the values above
     fit_hyperparameters: bool = True
     prior_set: str = "none"               # "none" (ScaleKernel(Linear + Matern) of Bayesian6/7) | "dim_scaled" | "gamma"
     mll_options: Optional[dict] = None    # scipy L-BFGS-B options
+    # with fixed hyperparameters: freeze the input standardisation at the first fit and fold each round's new rows in
+    # with the O(n^2 q) bordered update (gpx_append_f64) instead of refitting (Bayesian7.py:639 refits every round)
+    incremental_updates: bool = True
     # acquisition="qlogei": optimize_acqf settings of optimization/Bayesian.py:100-112
     mc_samples: int = 512
     num_restarts: int = 10
@@ -65,6 +78,64 @@ class GPConfig:
     maxiter: int = 200
 
 
+# ---- persistence -----------------------------------------------------------------------------------------------
+class _ResultsTable:
+    """results CSV (source of truth for resume) + validation log, in the reference's file formats."""
+
+    def __init__(self, directory: str, dim: int, num_outputs: int):
+        os.makedirs(directory, exist_ok=True)
+        self.path = os.path.join(directory, "optimization_results.csv")
+        self.metrics_path = os.path.join(directory, "validation_log.csv")
+        self.inputs = list(INPUT_COLUMNS[:dim])
+        self.outputs = [f"x_{k:02d}" for k in range(1, num_outputs + 1)]
+
+    @property
+    def columns(self) -> List[str]:
+        return self.inputs + self.outputs
+
+    def open(self, resume: bool) -> Optional[Tuple[np.ndarray, np.ndarray]]:
+        """Resume: the (X_phys, Y) rows already recorded, or None.  Fresh run: a new file with the header."""
+        rows = None
+        if resume and os.path.exists(self.path):
+            print(f"[resume] reading {self.path}")
+            try:
+                import pandas as pd
+
+                table = pd.read_csv(self.path)
+                if len(table):
+                    rows = (table[self.inputs].to_numpy(np.float64), table[self.outputs].to_numpy(np.float64))
+                    print(f"[resume] {len(table)} evaluations restored")
+            except Exception as err:  # a damaged file does not stop the run: start from what the model has
+                print(f"[resume] could not parse {self.path}: {err}")
+        else:
+            with open(self.path, "w", encoding="utf-8") as fh:
+                fh.write(",".join(self.columns) + "\n")
+        if not os.path.exists(self.metrics_path):
+            with open(self.metrics_path, "w", encoding="utf-8") as fh:
+                fh.write("iteration,dataset,mse,mae,max_err,r2\n")
+        return rows
+
+    def record(self, x_phys: np.ndarray, y: np.ndarray) -> None:
+        values = np.concatenate([np.asarray(x_phys, np.float64).ravel(), np.asarray(y, np.float64).ravel()])
+        with open(self.path, "a", encoding="utf-8") as fh:
+            fh.write(",".join("%.8f" % v for v in values) + "\n")
+
+    def record_metrics(self, n_train: int, name: str, per_output: np.ndarray) -> None:
+        r2, mse, mae, worst = per_output[:, 0], per_output[:, 1], per_output[:, 2], per_output[:, 3]
+        with open(self.metrics_path, "a", encoding="utf-8") as fh:
+            fh.write(f"{n_train},{name},{mse.mean():.6f},{mae.mean():.6f},{worst.max():.6f},{r2.mean():.4f}\n")
+
+    def read_validation(self, path: str) -> Optional[Tuple[np.ndarray, np.ndarray]]:
+        if not os.path.exists(path):
+            print(f"[validation] no test set at {path}")
+            return None
+        import pandas as pd
+
+        table = pd.read_csv(path).dropna(subset=self.columns)
+        return table[self.inputs].to_numpy(np.float64), table[self.outputs].to_numpy(np.float64)
+
+
+# ---- optimizer --------------------------------------------------------------------------------------------------
 class BayesianOptimizer:
     def __init__(
         self,
@@ -75,7 +146,7 @@ class BayesianOptimizer:
         n_batches: int,
         batch_size: int,
         num_outputs: int = 8,
-        svgp_threshold: int = 100,   # accepted for compatibility; the exact GP is used at every size
+        svgp_threshold: int = 100,   # accepted for compatibility: the exact GP serves every size
         resume: bool = False,
         target_total: Optional[int] = None,
         device: Optional[torch.device] = None,
@@ -83,324 +154,334 @@ class BayesianOptimizer:
         test_csv_path: Optional[str] = None,
         **kwargs,
     ):
-        self.engine = kwargs.pop("engine", None)
-        if self.engine is None:
-            self.engine = GPEngine(device)  # HIP path; raises if libgpx.so / the GPU is missing
+        engine = kwargs.pop("engine", None)
+        self.engine = engine if engine is not None else GPEngine(device)  # HIP path: raises without libgpx / a GPU
         self.gp_device = getattr(self.engine, "device", torch.device("cpu"))
         self.dtype = torch.float64
         self.config = gp_config or GPConfig()
         self.simulator = simulator
-        self.physical_bounds = np.asarray(bounds_list, dtype=np.float64)  # (D, 2)
-        self.dim = int(self.physical_bounds.shape[0])
+        box = np.asarray(bounds_list, dtype=np.float64)
+        self.physical_bounds = box
+        self._lo, self._span = box[:, 0], box[:, 1] - box[:, 0]
+        self.dim = box.shape[0]
         self.num_outputs = int(num_outputs)
-        self.n_initial_points = int(n_initial_points)
-        self.n_batches = int(n_batches)
-        self.batch_size = int(batch_size)
-        self.target_total = target_total
-        self.resume = resume
-        self.svgp_threshold = svgp_threshold
+        self.n_initial_points, self.n_batches, self.batch_size = int(n_initial_points), int(n_batches), int(batch_size)
+        self.target_total, self.resume, self.svgp_threshold = target_total, resume, svgp_threshold
         self.objective_mode = str(kwargs.get("objective_mode", "min")).lower()
         self.objective_index = kwargs.get("objective_index", None)
         self.objective_weights = kwargs.get("objective_weights", None)
         self.acquisition = str(kwargs.get("acquisition", "variance")).lower()
+        if self.acquisition not in ("variance", "logei", "ei", "ucb", "qlogei"):
+            raise ValueError(f"unknown acquisition '{self.acquisition}'")
         self.seed = kwargs.get("seed", None)
         self._rng = np.random.default_rng(self.seed)
 
+        self.table = _ResultsTable(output_dir, self.dim, self.num_outputs)
+        self.results_csv_path, self.val_log_path = self.table.path, self.table.metrics_path
+        self.model_save_path = os.path.join(output_dir, "exact_gp.pt")
         self.train_X = torch.empty((0, self.dim), dtype=self.dtype, device=self.gp_device)
         self.train_Y_raw = torch.empty((0, self.num_outputs), dtype=self.dtype, device=self.gp_device)
-        self.test_X = None
-        self.test_Y_raw = None
+        restored = self.table.open(resume)
+        if restored is not None:
+            self.train_X = self._tensor(self._to_unit(restored[0]))
+            self.train_Y_raw = self._tensor(restored[1])
+        self.test_X = self.test_Y_raw = None
+        if test_csv_path:
+            held_out = self.table.read_validation(test_csv_path)
+            if held_out is not None:
+                self.test_X, self.test_Y_raw = self._tensor(self._to_unit(held_out[0])), self._tensor(held_out[1])
         self.gp_model: Optional[ExactGP] = None
         self.x_tf: Optional[LogInputStandardizer] = None
         self.y_tf: Optional[LogOutputStandardizer] = None
         self.iteration_counter = 0
+        print(f"[gpx] exact-GP surrogate on {self.gp_device}, {self.num_outputs} outputs, acquisition={self.acquisition}")
 
-        os.makedirs(output_dir, exist_ok=True)
-        self.results_csv_path = os.path.join(output_dir, "optimization_results.csv")
-        self.val_log_path = os.path.join(output_dir, "validation_log.csv")
-        self.model_save_path = os.path.join(output_dir, "exact_gp.pt")
-        self._init_data()
-        if test_csv_path:
-            self._load_test_set(test_csv_path)
-        print(f"[BayesianOptimizer] Device: {self.gp_device} | exact GP (gpx) | outputs: {self.num_outputs}")
+    # -- units ---------------------------------------------------------------------------------------------------
+    def _tensor(self, a) -> torch.Tensor:
+        return torch.as_tensor(np.asarray(a, dtype=np.float64), device=self.gp_device)
 
-    # -- CSV init / resume (Bayesian7.py:268-293) --------------------------------------------------
-    def _cols(self):
-        return OUTPUT_COLS[: self.dim] + [f"x_{i:02d}" for i in range(1, self.num_outputs + 1)]
+    def _to_unit(self, x_phys: np.ndarray) -> np.ndarray:
+        return (np.asarray(x_phys, np.float64) - self._lo) / self._span
 
-    def _init_data(self):
-        cols = self._cols()
-        if os.path.exists(self.results_csv_path) and self.resume:
-            import pandas as pd
+    def _scaled_to_original(self, x_unit) -> np.ndarray:
+        u = x_unit.detach().cpu().numpy() if isinstance(x_unit, torch.Tensor) else np.asarray(x_unit)
+        return self._lo + u.reshape(-1).astype(np.float64) * self._span
 
-            print("[Resume] Loading existing CSV data...")
-            try:
-                df = pd.read_csv(self.results_csv_path)
-                if not df.empty:
-                    X_phys = df[cols[: self.dim]].to_numpy(dtype=np.float64)
-                    Y_raw = df[cols[self.dim:]].to_numpy(dtype=np.float64)
-                    b = self.physical_bounds
-                    X_unit = (X_phys - b[:, 0]) / (b[:, 1] - b[:, 0])
-                    self.train_X = torch.tensor(X_unit, dtype=self.dtype, device=self.gp_device)
-                    self.train_Y_raw = torch.tensor(Y_raw, dtype=self.dtype, device=self.gp_device)
-                    print(f"  -> Loaded {len(df)} samples.")
-            except Exception as e:  # reference: print and continue fresh
-                print(f"[Resume] Failed to load CSV: {e}")
-        else:
-            with open(self.results_csv_path, "w", encoding="utf-8") as f:
-                f.write(",".join(cols) + "\n")
-        if not os.path.exists(self.val_log_path):
-            with open(self.val_log_path, "w", encoding="utf-8") as f:
-                f.write("iteration,dataset,mse,mae,max_err,r2\n")
+    def _bounds_t(self) -> torch.Tensor:
+        return self._tensor(self.physical_bounds.T)
 
-    def _load_test_set(self, path: str):
-        if not os.path.exists(path):
-            print(f"[Validation] Test CSV not found: {path}")
-            return
-        import pandas as pd
-
-        df = pd.read_csv(path)
-        cols = self._cols()
-        df = df.dropna(subset=cols)
-        b = self.physical_bounds
-        X_unit = (df[cols[: self.dim]].to_numpy(dtype=np.float64) - b[:, 0]) / (b[:, 1] - b[:, 0])
-        self.test_X = torch.tensor(X_unit, dtype=self.dtype, device=self.gp_device)
-        self.test_Y_raw = torch.tensor(df[cols[self.dim:]].to_numpy(dtype=np.float64), dtype=self.dtype,
-                                       device=self.gp_device)
-
-    def _save_row(self, x_phys: np.ndarray, y_vals: np.ndarray):
-        row = np.concatenate([x_phys, y_vals])
-        with open(self.results_csv_path, "a", encoding="utf-8") as f:
-            f.write(",".join([f"{v:.8f}" for v in row]) + "\n")
-
-    # -- simulation wrapper (Bayesian7.py:330-352) --------------------------------------------------
+    # -- black-box evaluation ------------------------------------------------------------------------------------
     def run_simulation(self, params) -> Optional[np.ndarray]:
-        x_unit = params.detach().cpu().numpy().flatten() if isinstance(params, torch.Tensor) else \
-            np.asarray(params).flatten()
-        b = self.physical_bounds
-        x_phys = b[:, 0] + x_unit * (b[:, 1] - b[:, 0])
+        """One simulator call at a unit-cube point; any failure (exception, None, out-of-range geometry) -> None, like
+        the reference's wrapper (Bayesian7.py:330-352).  Width/height are the last two physical parameters."""
+        x = self._scaled_to_original(params)
         try:
-            self.simulator.configure_geometry(float(x_phys[3]), float(x_phys[4]))
-            disp = self.simulator.run_simulation(float(x_phys[0]), float(x_phys[1]), float(x_phys[2]))
-            if disp is None:
-                return None
-            disp = np.array(disp, dtype=np.float64).flatten()
-            if len(disp) < self.num_outputs:
-                disp = np.pad(disp, (0, self.num_outputs - len(disp)))
-            return disp[: self.num_outputs]
+            self.simulator.configure_geometry(float(x[3]), float(x[4]))
+            out = self.simulator.run_simulation(float(x[0]), float(x[1]), float(x[2]))
         except Exception:
             return None
+        if out is None:
+            return None
+        out = np.asarray(out, dtype=np.float64).ravel()[: self.num_outputs]
+        return np.pad(out, (0, self.num_outputs - out.size))
 
-    def _scaled_to_original(self, x_unit: torch.Tensor) -> np.ndarray:
-        b = self.physical_bounds
-        return x_unit.detach().cpu().numpy().flatten() * (b[:, 1] - b[:, 0]) + b[:, 0]
+    def _observe(self, x_unit: torch.Tensor) -> bool:
+        y = self.run_simulation(x_unit)
+        if y is None:
+            return False
+        self.train_X = torch.cat([self.train_X, x_unit.reshape(1, -1).to(self.train_X)])
+        self.train_Y_raw = torch.cat([self.train_Y_raw, self._tensor(y).reshape(1, -1)])
+        self.table.record(self._scaled_to_original(x_unit), y)
+        return True
 
-    # -- model ---------------------------------------------------------------------------------------
-    def _bounds_t(self):
-        return torch.tensor(self.physical_bounds.T, dtype=self.dtype, device=self.gp_device)
-
+    # -- surrogate -----------------------------------------------------------------------------------------------
     def _kernel_params(self) -> KernelParams:
         c = self.config
         return KernelParams(c.kernel, c.lengthscale, outputscale=c.outputscale, noise=c.noise,
                             linear_variance=c.linear_variance)
 
     def fit_gp_model(self):
-        """Transforms (Bayesian7.py:363-385) + one exact posterior update on the engine for all outputs."""
-        if self.train_X.shape[0] < 1:
-            raise RuntimeError("Need at least one observation.")
-        self.x_tf = LogInputStandardizer(self._bounds_t()).fit(self.train_X)
+        """Log-standardise (Bayesian7.py:363-385) and build the exact posterior for all outputs on the engine: a fresh
+        fit (hyperparameters by marginal likelihood, or fixed), or — fixed hyperparameters, incremental mode — the
+        previous round's factor extended by the rows observed since."""
+        n = self.train_X.shape[0]
+        if n < 1:
+            raise RuntimeError("fit_gp_model needs at least one observation")
+        cfg = self.config
+        grow = (not cfg.fit_hyperparameters and cfg.incremental_updates and self.gp_model is not None
+                and self.x_tf is not None and self.gp_model.train_X.shape[0] < n)
         self.y_tf = LogOutputStandardizer().fit(self.train_Y_raw)
-        Xs = self.x_tf(self.train_X)
         Ys = self.y_tf(self.train_Y_raw)
-        self.gp_model = ExactGP(Xs, Ys, self._kernel_params(), engine=self.engine,
-                                jitter_schedule=(0.0, self.config.jitter_val, 1e-2))
-        if self.config.fit_hyperparameters:
-            self.gp_model.fit_hyperparameters(self.config.prior_set, options=self.config.mll_options)
+        if grow:
+            n_old = self.gp_model.train_X.shape[0]
+            self.gp_model.train_Y = Ys[:n_old]  # re-standardised targets; alpha is recomputed from all of them
+            self.gp_model.append_observations(self.x_tf(self.train_X[n_old:]), Ys[n_old:])
+            return self.gp_model
+        self.x_tf = LogInputStandardizer(self._bounds_t()).fit(self.train_X)
+        self.gp_model = ExactGP(self.x_tf(self.train_X), Ys, self._kernel_params(), engine=self.engine,
+                                jitter_schedule=(0.0, cfg.jitter_val, 1e-2))
+        if cfg.fit_hyperparameters:
+            self.gp_model.fit_hyperparameters(cfg.prior_set, options=cfg.mll_options)
         else:
             self.gp_model.fit()
         return self.gp_model
 
     def predict(self, x_orig_numpy: np.ndarray, return_var: bool = False):
-        """Posterior mean of the outputs at physical-unit inputs (Bayesian2.predict, :146-174)."""
+        """Posterior mean of every output at physical-unit inputs, in physical units (Bayesian2.predict, :146-174)."""
         if self.gp_model is None:
             self.fit_gp_model()
-        x = torch.as_tensor(np.atleast_2d(np.asarray(x_orig_numpy, dtype=np.float64)), device=self.gp_device)
-        x_unit = (x - self._bounds_t()[0]) / (self._bounds_t()[1] - self._bounds_t()[0])
+        x_unit = self._tensor(self._to_unit(np.atleast_2d(np.asarray(x_orig_numpy, np.float64))))
         post = self.gp_model.posterior(self.x_tf(x_unit))
-        y = self.y_tf.inverse_mean(post.mean)
-        if return_var:
-            return y.cpu().numpy(), post.variance.cpu().numpy()
-        return y.cpu().numpy()
+        mean = self.y_tf.inverse_mean(post.mean).cpu().numpy()
+        return (mean, post.variance.cpu().numpy()) if return_var else mean
 
     def evaluate_model(self, X_unit: torch.Tensor, Y_true_raw: torch.Tensor, dataset_name: str = "Vali"):
-        """R2 / MSE / MAE / MaxErr per output, appended to validation_log.csv (Bayesian7.py:543-592)."""
+        """Per-output R2 / MSE / MAE / max error of the posterior mean (Bayesian7.py:543-592 reports the same four),
+        logged to validation_log.csv; returns the (T, 4) array."""
         if self.gp_model is None or X_unit is None or len(X_unit) == 0:
             return None
-        post = self.gp_model.posterior(self.x_tf(X_unit))
-        yp = self.y_tf.inverse_mean(post.mean).cpu().numpy()
-        yt = Y_true_raw.cpu().numpy()
-        rows = []
-        for i in range(self.num_outputs):
-            var = np.var(yt[:, i])
-            ss_res = float(((yt[:, i] - yp[:, i]) ** 2).sum())
-            r2 = 1.0 - ss_res / (var * len(yt)) if var > 1e-9 else 0.0
-            err = np.abs(yt[:, i] - yp[:, i])
-            rows.append((r2, float((err ** 2).mean()), float(err.mean()), float(err.max())))
-        arr = np.array(rows)
-        print(f"--- {dataset_name} Performance: mean R2={arr[:, 0].mean():.4f} MSE={arr[:, 1].mean():.4g}")
-        with open(self.val_log_path, "a", encoding="utf-8") as f:
-            f.write(f"{len(self.train_X)},{dataset_name},{arr[:, 1].mean():.6f},{arr[:, 2].mean():.6f},"
-                    f"{arr[:, 3].max():.6f},{arr[:, 0].mean():.4f}\n")
-        return arr
+        truth = Y_true_raw.cpu().numpy()
+        pred = self.y_tf.inverse_mean(self.gp_model.posterior(self.x_tf(X_unit)).mean).cpu().numpy()
+        resid = truth - pred
+        centred = truth - truth.mean(axis=0)
+        ss_tot = (centred ** 2).sum(axis=0)
+        r2 = np.where(ss_tot > 1e-9 * len(truth), 1.0 - (resid ** 2).sum(axis=0) / np.maximum(ss_tot, 1e-300), 0.0)
+        table = np.stack([r2, (resid ** 2).mean(axis=0), np.abs(resid).mean(axis=0), np.abs(resid).max(axis=0)], 1)
+        print(f"[{dataset_name}] n={len(truth)}  R2 {table[:, 0].mean():.4f}  MSE {table[:, 1].mean():.4g}")
+        if table[:, 0].mean() < 0.85 and dataset_name.lower().startswith("train"):
+            print(f"[{dataset_name}] low training R2: the surrogate underfits (check noise level / hyperparameters)")
+        self.table.record_metrics(len(self.train_X), dataset_name, table)
+        return table
 
-    # -- acquisition -----------------------------------------------------------------------------
-    def _lhs(self, n: int) -> np.ndarray:
+    # -- objective -----------------------------------------------------------------------------------------------
+    def _scalar_objective(self, Y_raw: torch.Tensor) -> torch.Tensor:
+        """What optimize() ranks observations by (Bayesian7.py:597-609)."""
+        if Y_raw is None or Y_raw.numel() == 0:
+            return torch.empty((0,), device=self.gp_device, dtype=self.dtype)
+        return Y_raw @ self._objective_weights(Y_raw)
+
+    _compute_objective = _scalar_objective  # the reference's name
+
+    def _objective_weights(self, like: Optional[torch.Tensor] = None) -> torch.Tensor:
+        T = self.num_outputs
+        if self.objective_weights is not None:
+            w = torch.as_tensor(self.objective_weights, dtype=torch.float64).reshape(-1)
+            if w.numel() != T:
+                raise ValueError(f"objective_weights needs {T} entries")
+        elif self.objective_index is not None:
+            w = torch.zeros(T, dtype=torch.float64)
+            w[int(self.objective_index)] = 1.0
+        else:
+            w = torch.ones(T, dtype=torch.float64)
+        return w.to(like.device if like is not None else self.gp_device)
+
+    def _acq_weights(self) -> torch.Tensor:
+        """Objective weights in the maximised direction (min mode negates), over the modelled outputs."""
+        sign = 1.0 if self.objective_mode == "max" else -1.0
+        return sign * self._objective_weights()
+
+    def _incumbent(self, w: torch.Tensor) -> float:
+        return float((self.y_tf(self.train_Y_raw) @ w.to(self.train_Y_raw)).max())
+
+    # -- acquisition ---------------------------------------------------------------------------------------------
+    def _latin_hypercube(self, n: int) -> np.ndarray:
         from scipy.stats import qmc
 
         return qmc.LatinHypercube(d=self.dim, seed=self._rng).random(n=n)
 
-    def _sobol(self, n: int) -> np.ndarray:
+    def _sobol_grid(self, n: int) -> np.ndarray:
         from scipy.stats import qmc
 
-        return qmc.Sobol(self.dim, scramble=True, seed=self._rng).random_base2(int(math.ceil(math.log2(max(n, 2)))))[:n]
-
-    def _objective_alpha(self):
-        """alpha and (y_mean, y_scale) of the scalar objective in the log-standardised space: one output
-        (objective_index) or output 0."""
-        t = int(self.objective_index) if self.objective_index is not None else 0
-        return t
+        pts = qmc.Sobol(self.dim, scramble=True, seed=self._rng).random_base2(max(1, math.ceil(math.log2(max(n, 2)))))
+        return pts[:n]
 
     def acquire(self, k: int) -> torch.Tensor:
-        """Select k unit-cube points.  variance mode: pool scan -> top-K_big -> FPS (Bayesian7.py:646-688);
-        improvement modes: analytic sweep over a Sobol grid, best k distinct scores (Bayesian.py:96-113)."""
-        gp = self.gp_model
+        """k unit-cube points to evaluate next (mode: see the module docstring)."""
+        k = int(k)
+        if k < 1:
+            return torch.empty((0, self.dim), dtype=self.dtype, device=self.gp_device)
         if self.acquisition == "variance":
-            pool = torch.tensor(self._lhs(self.config.candidates_pool_size), dtype=self.dtype, device=self.gp_device)
-            _, _, scores = gp.engine.acquire(gp.state, self.x_tf(pool), "variance", return_scores=True)
-            k_big = int(min(max(5000, 20 * k), self.config.K_BIG_CAP, self.config.candidates_pool_size))
-            k_big = max(min(k_big, pool.shape[0]), k)
-            _, idx_big = torch.topk(scores, k_big)
-            return farthest_point_sampling(pool[idx_big], k, self._rng)
+            return self._pool_scan(k)
         if self.acquisition == "qlogei":
             return self._acquire_qlogei(k)
-        grid = torch.tensor(self._sobol(self.config.raw_samples), dtype=self.dtype, device=self.gp_device)
-        t = self._objective_alpha()
-        # maximise the objective in log-standardised space; "min" mode flips the sign of the incumbent search
-        Ys = self.y_tf(self.train_Y_raw)[:, t]
-        sign = 1.0 if self.objective_mode == "max" else -1.0
-        alpha = sign * gp.state.alpha[:, t]
-        best_f = float((sign * Ys).max())
-        _, _, scores = gp.engine.acquire(gp.state, self.x_tf(grid), self.acquisition, best_f=best_f,
-                                         beta=self.config.beta, alpha=alpha, return_scores=True)
-        k = min(k, grid.shape[0])
-        _, idx = torch.topk(scores, k)
-        return grid[idx]
+        return self._analytic_sweep(k)
+
+    def _pool_scan(self, k: int) -> torch.Tensor:
+        """Bayesian7.py:650-686 on the device: pool -> summed variance -> top-K_big -> FPS(k) from a random start."""
+        cfg = self.config
+        gp = self.gp_model
+        pool = self._tensor(self._latin_hypercube(cfg.candidates_pool_size))
+        _, _, score = gp.engine.acquire(gp.state, self.x_tf(pool), "variance", return_scores=True)
+        # every output's variance is var_std * s_t^2 with s_t = 1 in the log-standardised space: the summed score
+        # ranks like the shared variance
+        k_big = min(max(5000, 20 * k), cfg.K_BIG_CAP, pool.shape[0])
+        _, order = self.engine.topk(score, k_big)
+        shortlist = pool[order.to(pool.device)]
+        if k >= k_big:  # FPS of at least all points keeps them all (Bayesian7.py:88-89)
+            return shortlist
+        start = int(self._rng.integers(0, k_big))
+        return shortlist[self.engine.fps(shortlist, k, start).to(pool.device)]
+
+    def _objective_sweep_args(self, w: torch.Tensor) -> dict:
+        """(alpha, y_mean, y_scale) that make the engine's sweep score the objective sum_t w_t f_t (f_t the modelled
+        outputs, sharing the covariance and the constant mean c): mean c sum(w) + k*^T sum_t w_t alpha_t, variance
+        |w|^2 var.  The engine computes y_mean + y_scale (c + k*^T alpha'), y_scale^2 var, hence
+        y_scale = |w|, alpha' = sum_t w_t alpha_t / |w|, y_mean = c (sum(w) - |w|)."""
+        st = self.gp_model.state
+        w = w.to(device=st.alpha.device, dtype=torch.float64)
+        s = float(torch.linalg.vector_norm(w))
+        if s == 0.0:
+            raise ValueError("objective weights are all zero")
+        c = float(st.params.const_mean)
+        alpha = (st.alpha[:, : w.numel()] @ w) / s
+        return {"alpha": alpha.contiguous(), "y_mean": c * (float(w.sum()) - s), "y_scale": s}
+
+    def _analytic_sweep(self, k: int) -> torch.Tensor:
+        gp = self.gp_model
+        grid = self._tensor(self._sobol_grid(self.config.raw_samples))
+        w = self._acq_weights()
+        _, _, score = gp.engine.acquire(gp.state, self.x_tf(grid), self.acquisition, best_f=self._incumbent(w),
+                                        beta=self.config.beta, return_scores=True, **self._objective_sweep_args(w))
+        _, order = self.engine.topk(score, min(k, grid.shape[0]))
+        return grid[order.to(grid.device)]
 
     def _acquire_qlogei(self, k: int) -> torch.Tensor:
-        """optimize_acqf on MC qLogEI with q = k jointly (optimization/Bayesian.py:96-113: 512 Sobol base samples,
-        num_restarts 10, raw_samples 1024, batch_limit 5, maxiter 200), through the log-input transform, in the
-        log-standardised output space (acqf.py)."""
+        """optimize_acqf on MC qLogEI (Bayesian.py:96-113: 512 Sobol base samples, 10 restarts, 1024 raw samples,
+        batch_limit 5, maxiter 200) in the unit cube through the log-input transform.  Chunks of at most GPX_MAX_Q
+        points; after each, the model is conditioned on the chunk with its posterior mean (kriging believer)."""
         from .acqf import LinearMCObjective, SobolQMCNormalSampler, optimize_acqf, qLogExpectedImprovement
 
-        gp = self.gp_model
-        t = self._objective_alpha()
-        sign = 1.0 if self.objective_mode == "max" else -1.0
-        Ys = self.y_tf(self.train_Y_raw)[:, t]
-        w = [0.0] * gp.num_outputs
-        w[t] = sign
-        seed = int(self._rng.integers(0, 1 << 30))
-        acq = qLogExpectedImprovement(gp, best_f=float((sign * Ys).max()),
-                                      sampler=SobolQMCNormalSampler(torch.Size([self.config.mc_samples]), seed),
-                                      objective=LinearMCObjective(w))
+        cfg = self.config
+        w = self._acq_weights()
+        best_f = self._incumbent(w)
+        objective = LinearMCObjective(w.cpu())
+        unit_box = torch.stack([torch.zeros(self.dim), torch.ones(self.dim)]).to(self.dtype)
         x_tf = self.x_tf
+        model = self.gp_model
+        picked: List[torch.Tensor] = []
+        remaining = k
+        while remaining > 0:
+            q = min(remaining, _capi.GPX_MAX_Q)
+            seed = int(self._rng.integers(0, 1 << 30))
+            acq = qLogExpectedImprovement(model, best_f=best_f, objective=objective,
+                                          sampler=SobolQMCNormalSampler(torch.Size([cfg.mc_samples]), seed))
 
-        class _OnUnitCube:  # the GP sees transformed inputs; optimize_acqf works in the unit cube
-            model = gp
+            class _UnitCube:  # optimize_acqf searches the unit cube; the GP sees transformed inputs
+                def __init__(self, inner, m):
+                    self.inner, self.model = inner, m
 
-            def __call__(self, X):
-                return acq(x_tf(X.reshape(-1, X.shape[-1])).reshape(X.shape))
+                def __call__(self, X):
+                    return self.inner(x_tf(X.reshape(-1, X.shape[-1])).reshape(X.shape))
 
-        bounds = torch.stack([torch.zeros(self.dim), torch.ones(self.dim)]).to(self.dtype)
-        cand, _ = optimize_acqf(_OnUnitCube(), bounds, q=k, num_restarts=self.config.num_restarts,
-                                raw_samples=self.config.acqf_raw_samples,
-                                options={"batch_limit": self.config.batch_limit, "maxiter": self.config.maxiter},
-                                seed=seed)
-        return cand.detach()
+            cand, _ = optimize_acqf(_UnitCube(acq, model), unit_box, q=q, num_restarts=cfg.num_restarts,
+                                    raw_samples=cfg.acqf_raw_samples,
+                                    options={"batch_limit": cfg.batch_limit, "maxiter": cfg.maxiter}, seed=seed)
+            cand = cand.detach().reshape(q, self.dim)
+            picked.append(cand)
+            remaining -= q
+            if remaining > 0:  # condition on the chunk: fantasy observations = current posterior means
+                Xf = x_tf(cand.to(self.gp_device))
+                fantasy = model.posterior(Xf).mean
+                model = ExactGP(torch.cat([model.train_X, Xf]), torch.cat([model.train_Y, fantasy]), model.params,
+                                engine=self.engine, jitter_schedule=model.jitter_schedule).fit()
+        return torch.cat(picked)
 
     def optimize_acquisition_function(self, gp=None) -> torch.Tensor:
         return self.acquire(self.batch_size)
 
-    # -- objective / main loop (Bayesian7.py:597-733) ---------------------------------------------
-    def _compute_objective(self, Y_raw: torch.Tensor) -> torch.Tensor:
-        if Y_raw is None or Y_raw.numel() == 0:
-            return torch.empty((0,), device=self.gp_device, dtype=self.dtype)
-        if self.objective_weights is not None:
-            w = torch.tensor(self.objective_weights, device=Y_raw.device, dtype=Y_raw.dtype).view(1, -1)
-            return (Y_raw * w).sum(dim=1)
-        if self.objective_index is not None:
-            return Y_raw[:, int(self.objective_index)]
-        return Y_raw.sum(dim=1)
+    # -- main loop -----------------------------------------------------------------------------------------------
+    def _initial_design(self):
+        missing = self.n_initial_points - self.train_X.shape[0]
+        if missing <= 0:
+            return
+        print(f"[init] Latin-hypercube design of {missing} points")
+        for row in self._latin_hypercube(missing):
+            self._observe(self._tensor(row))
 
-    def _append(self, x_u: torch.Tensor, disp: np.ndarray):
-        self.train_X = torch.cat([self.train_X, x_u.reshape(1, -1).to(self.train_X)])
-        self.train_Y_raw = torch.cat([self.train_Y_raw, torch.tensor(disp, device=self.gp_device,
-                                                                     dtype=self.dtype).reshape(1, -1)])
-        self._save_row(self._scaled_to_original(x_u), disp)
-
-    def optimize(self):
-        assert self.target_total is not None, "target_total must be provided (e.g., 100000)"
-        print("[BayesianOptimizer] Starting optimization...")
-        if self.train_X.shape[0] < self.n_initial_points:
-            print(f"[Init] Collecting {self.n_initial_points} LHS points...")
-            for s in self._lhs(self.n_initial_points - self.train_X.shape[0]):
-                x_u = torch.tensor(s, dtype=self.dtype, device=self.gp_device)
-                disp = self.run_simulation(x_u)
-                if disp is not None:
-                    self._append(x_u, disp)
-        while len(self.train_X) < self.target_total:
-            self.iteration_counter += 1
-            print(f"\n=== Iteration: {len(self.train_X)} samples ===")
-            self.fit_gp_model()
-            self.evaluate_model(self.train_X, self.train_Y_raw, "Train_Set")
-            if self.test_X is not None:
-                self.evaluate_model(self.test_X, self.test_Y_raw, "Test_Set")
-            batch_k = min(self.config.acq_batch_size, self.batch_size, self.target_total - len(self.train_X))
-            batch_X = self.acquire(batch_k)
-            print(f"[Acquisition] Selected {len(batch_X)} points ({self.acquisition}).")
-            new_cnt = 0
-            for x_u in batch_X:
-                disp = self.run_simulation(x_u)
-                if disp is not None:
-                    self._append(x_u, disp)
-                    new_cnt += 1
-            if new_cnt == 0:
-                print("[Stop] No valid simulations returned in this batch.")
-                break
-            try:
+    def _round(self) -> int:
+        """One active-learning round: fit, report, select (Bayesian7.py:676: min(acq_batch_size, remaining) points),
+        evaluate.  Returns the number of successful evaluations."""
+        self.iteration_counter += 1
+        print(f"\n[round {self.iteration_counter}] {len(self.train_X)} observations")
+        self.fit_gp_model()
+        self.evaluate_model(self.train_X, self.train_Y_raw, "Train_Set")
+        if self.test_X is not None:
+            self.evaluate_model(self.test_X, self.test_Y_raw, "Test_Set")
+        want = min(self.config.acq_batch_size, self.target_total - len(self.train_X))
+        batch = self.acquire(want)
+        print(f"[round {self.iteration_counter}] {len(batch)} points selected by {self.acquisition}")
+        ok = sum(self._observe(x) for x in batch)
+        if ok:
+            try:  # the model is recomputable from the CSV; this snapshot is a convenience
                 torch.save({"X": self.train_X.cpu(), "Y": self.train_Y_raw.cpu(),
-                            "kernel": self._kernel_params().__dict__}, self.model_save_path)
+                            "kernel": dict(self.gp_model.params.__dict__)}, self.model_save_path)
             except Exception:
                 pass
-        print("[Done] Optimization finished.")
-        if self.train_X.shape[0] == 0:
+        return ok
+
+    def optimize(self):
+        if self.target_total is None:
+            raise AssertionError("optimize() needs target_total (the total number of evaluations to reach)")
+        self._initial_design()
+        while len(self.train_X) < self.target_total:
+            if self._round() == 0:
+                print("[stop] every simulation of the round failed")
+                break
+        print(f"[done] {len(self.train_X)} evaluations")
+        if len(self.train_X) == 0:
             return None, None
-        obj = self._compute_objective(self.train_Y_raw)
-        best_idx = int(torch.argmax(obj).item()) if self.objective_mode == "max" else int(torch.argmin(obj).item())
-        return self._scaled_to_original(self.train_X[best_idx]), float(obj[best_idx].item())
+        obj = self._scalar_objective(self.train_Y_raw)
+        best = int(torch.argmax(obj)) if self.objective_mode == "max" else int(torch.argmin(obj))
+        return self._scaled_to_original(self.train_X[best]), float(obj[best])
 
 
-def farthest_point_sampling(X: torch.Tensor, m: int, rng: Optional[np.random.Generator] = None) -> torch.Tensor:
-    """Greedy farthest-point sampling (Bayesian7.py:82-106) on the tensor's device, one sync at the end."""
+def farthest_point_sampling(X: torch.Tensor, m: int, rng: Optional[np.random.Generator] = None,
+                            engine: Optional[GPEngine] = None) -> torch.Tensor:
+    """The m rows of X chosen by greedy farthest-point sampling from a random start (Bayesian7.py:82-106), on the
+    device through gpx_fps_f64 (``engine`` defaults to one on X's device)."""
     n = X.shape[0]
     if m >= n:
         return X
     rng = rng or np.random.default_rng()
-    idx = torch.empty(m, dtype=torch.long, device=X.device)
-    first = int(rng.integers(0, n))
-    idx[0] = first
-    dists = torch.linalg.vector_norm(X - X[first], dim=1)
-    for t in range(1, m):
-        nxt = torch.argmax(dists)
-        idx[t] = nxt
-        dists = torch.minimum(dists, torch.linalg.vector_norm(X - X[nxt], dim=1))
-    return X[idx]
+    eng = engine if engine is not None else GPEngine(X.device)
+    return X[eng.fps(X, m, int(rng.integers(0, n)))]

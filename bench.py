@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from bayesianoptimizer_amd import GPEngine, KernelParams, botorch_default_lengthscale, synthetic  # noqa: E402
+from bayesianoptimizer_amd.dist import RCCLArgmaxExchange  # noqa: E402
 
 METRIC = "GP posterior updates/sec + acq-cands/sec, n=4096 d=8 fp64, 1→8 MI355X"
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix, spec; measured 78.1 TF/s (profiles/r01_probe_f64_rate.log)
@@ -119,7 +120,7 @@ def _torch_cpu_step(X, y, Xs, ls, noise, best_f, kind):
     return best
 
 
-def cpu_baseline(X, y, Xs_np, kind, acq, ls, sample, reps=3):
+def cpu_baseline(X, y, Xs_np, kind, acq, ls, sample, reps=5):
     """CPU baseline on the host cores, two restatements of the same step, the faster one reported:
     the NumPy/SciPy oracle (one fit + a sweep over `sample` candidates) and torch-CPU fp64 (median of `reps`
     after a warm-up, over 8x the sample).  Each is extrapolated linearly from its sample to the full step."""
@@ -256,6 +257,52 @@ def other_configs(eng, dev, seed):
         "best_index": int(bi.item())}
     del st, X, y, Xs
     torch.cuda.empty_cache()
+    # BASELINE configs[3] at its per-GPU share (32 restarts over 8 GPUs = 4 per GPU): 4 independent n = 4096 d = 8 RBF
+    # problems fitted in the same launches (gpx_fit_batched_f64), a 2^20-candidate logEI sweep each and the local
+    # combine of their records (the cross-GPU exchange is the --gpus N path of the headline line)
+    P4 = 4
+    pr = [synthetic.problem(4096, 8, seed + 100 + q) for q in range(P4)]
+    Xb = torch.tensor(np.stack([a for a, _ in pr]), device=dev)
+    yb = torch.tensor(np.stack([b for _, b in pr]), device=dev)
+    Xs4 = [torch.tensor(synthetic.sobol(1 << 20, 8, seed + 200 + q), device=dev) for q in range(P4)]
+    bf4 = [float(b.max()) for _, b in pr]
+    p = KernelParams("rbf", botorch_default_lengthscale(8), noise=1e-4)
+    sts = eng.fit_batched(Xb, yb, p)
+    lv = torch.empty((P4,), dtype=torch.float64, device=dev)
+    li = torch.empty((P4,), dtype=torch.int64, device=dev)
+
+    def share_step():
+        ss = eng.fit_batched(Xb, yb, p, check=False, out=sts)
+        for q in range(P4):
+            v, i = eng.acquire(ss[q], Xs4[q], "logei", best_f=bf4[q], index_offset=q << 20)
+            lv[q:q + 1].copy_(v)
+            li[q:q + 1].copy_(i)
+        return eng.argmax_combine(lv, li)
+
+    share_step()
+    tf, ts = [], []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        eng.fit_batched(Xb, yb, p, check=False, out=sts)
+        torch.cuda.synchronize()
+        tf.append(time.perf_counter() - a)
+    for _ in range(2):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        bv, bi = share_step()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - a)
+    if any(st.pivot_failure() >= 0 for st in sts):
+        raise RuntimeError("configs[3] share: Cholesky failed")
+    f, t = float(np.median(tf)), float(np.median(ts))
+    out["configs[3] per-GPU share"] = {
+        "workload": "4 independent n=4096 d=8 RBF fp64 problems per GPU (32 restarts / 8 GPUs), batched posterior "
+                    "update + a 1048576-candidate logEI sweep each + argmax combine",
+        "problems": P4, "batched_fit_ms": 1e3 * f, "updates_per_s": P4 / f, "ms_per_step": 1e3 * t,
+        "acq_cands_per_s": P4 * (1 << 20) / t, "best_index": int(bi.item())}
+    del sts, Xb, yb, Xs4
+    torch.cuda.empty_cache()
     # the BO loop's per-iteration update done incrementally: one new observation appended to an
     # n = 4096 fit by the bordered Cholesky (gpx_append_f64; the same factor a refit computes, GPU parity tests),
     # beside the headline's full refit
@@ -309,8 +356,9 @@ def main():
             return eng.fit_batched(Xb, yb, params, check=False, out=states)
         return [eng.fit(Xb[0], yb[0], params, check=False, out=states[0])]
 
-    gather_v = torch.empty((world,), dtype=torch.float64, device=dev)
-    gather_i = torch.empty((world,), dtype=torch.int64, device=dev)
+    # the cross-rank exchange through libgpx's own RCCL communicator (gpx_allreduce_argmax): one 16-byte record per
+    # rank, one all-gather, the deterministic combine kernel - no torch collective inside the timed step
+    exchange = RCCLArgmaxExchange(eng) if dist is not None else None
     loc_v = torch.empty((P,), dtype=torch.float64, device=dev)
     loc_i = torch.empty((P,), dtype=torch.int64, device=dev)
 
@@ -321,10 +369,8 @@ def main():
             loc_v[q:q + 1].copy_(bv)
             loc_i[q:q + 1].copy_(bi)
         bv, bi = eng.argmax_combine(loc_v, loc_i) if P > 1 else (loc_v[:1], loc_i[:1])
-        if dist is not None:
-            dist.all_gather_into_tensor(gather_v, bv)
-            dist.all_gather_into_tensor(gather_i, bi)
-            bv, bi = eng.argmax_combine(gather_v, gather_i)
+        if exchange is not None:
+            bv, bi = exchange(bv, bi)
         return bv, bi
 
     for _ in range(args.warmup):
@@ -430,6 +476,8 @@ def main():
             "other_configs": extra,
         }
         print(json.dumps(out))
+    if exchange is not None:
+        exchange.close()
     if dist is not None:
         dist.destroy_process_group()
 

@@ -99,12 +99,12 @@ typedef struct {
   int32_t cov_fp32;                      /* 1: evaluate distances / exp / Matérn polynomial in fp32 (BASELINE
                                             configs[4] mixed-precision build), widen to fp64 before the fp64
                                             factorisation and sweep; 0: fp64 throughout */
-  int32_t reserved;
+  int32_t reserved;                      /* must be 0 */
 } gpx_kernel_params;
 
 typedef struct {
   int32_t kind;     /* GPX_ACQ_* */
-  int32_t reserved;
+  int32_t reserved; /* must be 0 */
   double best_f;    /* incumbent, in untransformed units (optimization/Bayesian.py:98) */
   double beta;      /* UCB beta */
   double y_mean;    /* Standardize untransform: mu_out = y_mean + y_scale * mu */
@@ -119,6 +119,11 @@ gpx_status gpx_destroy(gpx_handle h);
 gpx_status gpx_set_stream(gpx_handle h, void* stream);
 const char* gpx_last_error(gpx_handle h);
 int64_t gpx_padded_n(int64_t n);
+/* sizeof(gpx_kernel_params) (560) and sizeof(gpx_acq_params) (40) as compiled into the library: a binding checks its
+ * own struct definitions against these once at load time.  Every entry point taking a
+ * gpx_kernel_params also rejects cov_fp32 outside {0, 1} and reserved != 0 with GPX_INVALID_ARG. */
+size_t gpx_kernel_params_size(void);
+size_t gpx_acq_params_size(void);
 
 /* ---- fit = posterior update ----------------------------------------------- */
 /* Gram K(X,X)+(noise+jitter)I into the lower triangle of the padded K (replaces the covar_module(X) +
@@ -234,9 +239,10 @@ gpx_status gpx_moments_grad_f64(gpx_handle h, const gpx_kernel_params* p, int64_
 /* ---- cross-GPU selection exchange (SURVEY §8b gpx_allreduce_argmax, §8e) ------------------------------------------ */
 /* One process per GPU.  Rank 0 creates the communicator id (gpx_comm_unique_id), the host side broadcasts its
  * GPX_COMM_ID_BYTES bytes (e.g. over torch.distributed), every rank calls gpx_comm_init (collective).
- * gpx_allreduce_argmax replaces every rank's device (best_val, best_idx) record by the global best: an RCCL
- * all-gather of the 16-byte records over xGMI, then the argmax_combine kernel (max value, lowest global index, NaN
- * never wins) on the handle's stream — RCCL has no MAXLOC.  Replaces the final best-candidate selection across the
+ * gpx_allreduce_argmax replaces every rank's device (best_val, best_idx) record by the global best: the record is
+ * packed into one 16-byte {fp64 value, int64 index} on the device, ONE RCCL all-gather of those 16 bytes per rank runs
+ * over xGMI, then the argmax_combine kernel (max value, lowest global index, NaN never wins) on the handle's stream —
+ * RCCL has no MAXLOC.  Three stream operations per exchange; no host synchronisation.  Replaces the final best-candidate selection across the
  * independent restarts/shards (BASELINE configs[3]). */
 gpx_status gpx_comm_unique_id(uint8_t* id_out);
 gpx_status gpx_comm_init(gpx_handle h, const uint8_t* id, int32_t nranks, int32_t rank, gpx_comm* out);

@@ -98,3 +98,24 @@ class OracleEngine:
     def argmax_combine(self, vals, idx):
         v, i = O.combine_argmax(list(zip(vals.tolist(), idx.tolist())))
         return torch.tensor([v]), torch.tensor([i])
+
+    def topk(self, scores, k):
+        self.calls["topk"] = self.calls.get("topk", 0) + 1
+        v, i = O.topk_desc(torch.as_tensor(scores).cpu().numpy(), int(k))
+        return torch.tensor(v), torch.tensor(i)
+
+    def fps(self, X, k, start):
+        self.calls["fps"] = self.calls.get("fps", 0) + 1
+        return torch.tensor(O.farthest_point_sampling(torch.as_tensor(X).cpu().numpy(), int(k), int(start)))
+
+    def append(self, state, X, Y, check=True):
+        self.calls["append"] = self.calls.get("append", 0) + 1
+        X = torch.as_tensor(X, dtype=torch.float64).cpu().numpy()
+        Y = torch.as_tensor(Y, dtype=torch.float64).cpu().numpy()
+        if Y.ndim == 1:
+            Y = Y[:, None]
+        try:
+            st = O.append(state.st, X, Y)
+        except O.NotPDError as e:
+            raise NotPositiveDefiniteError(e.pivot)
+        return OState(st, torch.tensor(st.alpha.reshape(X.shape[0], -1)), X.shape[0], Y.shape[1], state.params)

@@ -97,3 +97,41 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_capi, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(_capi.GPXLibraryError):
         _capi.load()
+
+
+def _integration_struct():
+    """The KernelParams class of INTEGRATION.md's ctypes binding snippet, executed as documented."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    block = re.search(r"```python\n(# optimization/gpx_binding\.py.*?)```", text, re.S).group(1)
+    start = block.index("class KernelParams(ctypes.Structure):")
+    cls = block[start:block.index("\n\n", start)]
+    ns = {"ctypes": ctypes}
+    exec(cls, ns)  # noqa: S102 - our own documentation
+    assert "assert ctypes.sizeof(KernelParams) == lib.gpx_kernel_params_size()" in block
+    return ns["KernelParams"]
+
+
+def test_integration_binding_struct_matches_header(lib):
+    doc = _integration_struct()
+    assert ctypes.sizeof(doc) == ctypes.sizeof(_capi.KernelParamsC) == lib.gpx_kernel_params_size() == 560
+    assert [f[0] for f in doc._fields_] == [f[0] for f in _capi.KernelParamsC._fields_]
+    for name, _ in _capi.KernelParamsC._fields_:
+        assert getattr(doc, name).offset == getattr(_capi.KernelParamsC, name).offset, name
+        assert getattr(doc, name).size == getattr(_capi.KernelParamsC, name).size, name
+    assert lib.gpx_acq_params_size() == ctypes.sizeof(_capi.AcqParamsC) == 40
+
+
+def test_truncated_struct_binding_is_refused(monkeypatch):
+    """A binding whose gpx_kernel_params stops before cov_fp32/reserved (the 552-byte struct of round 1's doc) is
+    refused at load instead of letting the library read past the caller's object."""
+    class Truncated(ctypes.Structure):
+        _fields_ = _capi.KernelParamsC._fields_[:-2]
+
+    assert ctypes.sizeof(Truncated) == 552
+    monkeypatch.setattr(_capi, "_lib", None)
+    monkeypatch.setattr(_capi, "KernelParamsC", Truncated)
+    with pytest.raises(_capi.GPXLibraryError, match="552 bytes, libgpx expects 560"):
+        _capi.load()
+    monkeypatch.undo()
+    _capi._lib = None
+    _capi.load()

@@ -414,6 +414,45 @@ def test_fit_batched_matches_single_fits_and_oracle(engine, n, B, nrhs):
         check_posterior(mu.cpu().numpy(), var.cpu().numpy(), mu_r, var_r, O.kernel_diag(Xq, op))
 
 
+def test_configs3_per_gpu_share_batched_n4096(engine):
+    """BASELINE configs[3] (32 independent restarts x n=4096 d=8 over 8 GPUs) at its per-GPU share: 4 problems fitted in
+    the same launches (gpx_fit_batched_f64), each bit-identical to its own single fit, each with a 2^20-candidate logEI
+    sweep checked by the full-size properties (device argmax = argmax of its scores, oracle re-score of the top-64 plus
+    random candidates agrees on the winner and the values), then the records combined like the cross-GPU exchange
+    (per-restart selection of optimize_acqf, /root/reference/optimization/Bayesian.py:105-112)."""
+    n, d, m, B = 4096, 8, 1 << 20, 4
+    kp, op = pair("rbf", d, noise=1e-4)
+    probs = [O.synthetic_problem(n, d, 1000 * b) for b in range(B)]
+    sts = engine.fit_batched(t(np.stack([p[0] for p in probs])), t(np.stack([p[1] for p in probs])), kp)
+    vals, idxs = [], []
+    for b, (X, y) in enumerate(probs):
+        single = engine.fit(t(X), t(y), kp)
+        assert torch.equal(torch.tril(sts[b].L), torch.tril(single.L))
+        assert torch.equal(torch.triu(sts[b].W), torch.triu(single.W))
+        assert torch.equal(sts[b].alpha, single.alpha)
+        del single
+        Xs = O.sobol_candidates(m, d, 1000 * b + 1)
+        best_f = float(y.max())
+        bv, bi, sc = engine.acquire(sts[b], t(Xs), "logei", best_f=best_f, index_offset=b * m, return_scores=True)
+        sg = sc.cpu().numpy()
+        assert np.isfinite(sg).all()
+        assert int(bi.item()) == b * m + int(np.argmax(sg))
+        top = np.argsort(-sg)[:64]
+        rnd = np.random.default_rng(b).choice(m, 1024, replace=False)
+        sel = np.unique(np.concatenate([top, rnd]))
+        ost = O.fit(X, y, op)
+        mu, var = O.posterior(ost, Xs[sel])
+        sref = O.acquisition(mu, var, O.ACQ_LOGEI, best_f)
+        assert b * m + sel[int(np.argmax(sref))] == int(bi.item())
+        ok = (mu - best_f) / np.sqrt(var) > -10
+        assert np.abs(sg[sel][ok] - sref[ok]).max() <= 1e-8 * max(1.0, np.abs(sref[ok]).max())
+        vals.append(float(bv.item()))
+        idxs.append(int(bi.item()))
+    gv, gi = engine.argmax_combine(torch.tensor(vals, dtype=torch.float64), torch.tensor(idxs))
+    ref_v, ref_i = O.combine_argmax(list(zip(vals, idxs)))
+    assert (float(gv.item()), int(gi.item())) == (ref_v, ref_i)
+
+
 def test_fit_batched_reports_not_pd_per_problem(engine):
     n, d, B = 200, 3, 3
     Xs = np.stack([O.synthetic_problem(n, d, 7 + b)[0] for b in range(B)])
@@ -508,3 +547,29 @@ def test_empty_and_non_finite_inputs(engine):
     assert np.isnan(s2[i0]) and np.array_equal(np.delete(s1, i0), np.delete(s2, i0))
     ref = np.delete(np.arange(500), i0)[int(np.argmax(np.delete(s1, i0)))]
     assert int(bi2.item()) == ref and float(bv2.item()) == s1[ref]
+
+
+def test_kernel_params_trailing_fields_are_validated(engine):
+    """cov_fp32 outside {0, 1} or a non-zero reserved word (what a truncated caller struct hands over) is rejected with
+    GPX_INVALID_ARG instead of silently switching the covariance build (include/gpx.h)."""
+    import ctypes
+
+    from bayesianoptimizer_amd import _capi
+
+    X, _ = O.synthetic_problem(64, 3, 5)
+    Xt = t(X)
+    K = torch.zeros((128, 128), dtype=torch.float64, device=DEV)
+    kp, _ = pair("rbf", 3)
+    engine._bind_stream()
+
+    def gram(pc):
+        return engine.lib.gpx_gram_f64(engine.handle, ctypes.byref(pc), 64, ctypes.c_void_p(Xt.data_ptr()), 3,
+                                       ctypes.c_void_p(K.data_ptr()), 128)
+
+    pc = kp.to_c(3)
+    assert gram(pc) == _capi.GPX_OK
+    pc.cov_fp32 = 7
+    assert gram(pc) == _capi.GPX_INVALID_ARG and b"cov_fp32" in engine.lib.gpx_last_error(engine.handle)
+    pc.cov_fp32 = 0
+    pc.reserved = 1
+    assert gram(pc) == _capi.GPX_INVALID_ARG and b"reserved" in engine.lib.gpx_last_error(engine.handle)

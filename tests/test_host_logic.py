@@ -101,7 +101,7 @@ def test_jitter_retry_policy():
 
 def test_farthest_point_sampling_spreads():
     X = torch.tensor(O.sobol_candidates(256, 2, 0))
-    S = farthest_point_sampling(X, 8, np.random.default_rng(0))
+    S = farthest_point_sampling(X, 8, np.random.default_rng(0), engine=OracleEngine())
     assert S.shape == (8, 2)
     d = torch.cdist(S, S) + torch.eye(8) * 10
     assert float(d.min()) > 0.15
@@ -160,3 +160,70 @@ def test_product_default_engine_requires_gpu(tmp_path):
         pytest.skip("GPU present: the default engine is valid here")
     with pytest.raises(Exception):
         BayesianOptimizer(StubSimulator(), BOUNDS, str(tmp_path), 4, 1, 2, target_total=8)
+
+
+@pytest.mark.parametrize("mode", ["min", "max"])
+@pytest.mark.parametrize("acq", ["ei", "logei", "ucb"])
+def test_dropin_analytic_sweep_scores_the_reported_objective(tmp_path, mode, acq):
+    """The improvement sweep scores sum_t w_t f_t (w = +-objective weights) with the learned constant mean included
+    in every output (min mode used to negate alpha but not the constant mean, off by 2c)."""
+    eng = OracleEngine()
+    weights = [0.5, 1.0, 0.0, 2.0, 0.0, 0.0, 0.25, 1.0]
+    opt = BayesianOptimizer(StubSimulator(), BOUNDS, str(tmp_path), n_initial_points=30, n_batches=0, batch_size=4,
+                            target_total=30, engine=eng, seed=5, gp_config=GPConfig(fit_hyperparameters=False),
+                            acquisition=acq, objective_mode=mode, objective_weights=weights)
+    opt.optimize()
+    opt.fit_gp_model()
+    gp = opt.gp_model
+    gp.params = gp.params.replace(const_mean=0.37)  # a non-zero learned constant mean
+    gp.fit()
+    w = opt._acq_weights()
+    Xq = torch.tensor(O.sobol_candidates(64, 5, 9))
+    Xt = opt.x_tf(Xq)
+    best_f = opt._incumbent(w)
+    _, _, got = eng.acquire(gp.state, Xt, acq, best_f=best_f, beta=4.0, return_scores=True,
+                            **opt._objective_sweep_args(w))
+    # reference: per-output posteriors (each with the constant mean), combined
+    st = gp.state.st
+    wn = w.numpy()
+    mu = np.zeros(64)
+    for tt in range(8):
+        one = O.GPState(X=st.X, L=st.L, alpha=st.alpha.reshape(st.X.shape[0], -1)[:, tt], params=st.params)
+        mu_t, var_std = O.posterior(one, Xt.numpy())
+        mu += wn[tt] * mu_t
+    var = np.maximum(var_std * float((wn ** 2).sum()), O.BOTORCH_MIN_VAR)
+    ref = O.acquisition(mu, var, {"ei": O.ACQ_EI, "logei": O.ACQ_LOGEI, "ucb": O.ACQ_UCB}[acq], best_f, 4.0)
+    np.testing.assert_allclose(got.numpy(), ref, rtol=1e-9, atol=1e-12)
+    # and the incumbent is the best observed objective in the same units
+    Ys = opt.y_tf(opt.train_Y_raw).numpy()
+    assert best_f == pytest.approx(float((Ys @ wn).max()), rel=1e-12)
+
+
+def test_dropin_qlogei_larger_than_joint_q_limit(tmp_path):
+    """acquisition="qlogei" with a batch above GPX_MAX_Q (the reference driver's default batch is 1000): greedy chunks
+    of at most 32 points on kriging-believer fantasy models."""
+    cfg = GPConfig(mc_samples=16, num_restarts=1, acqf_raw_samples=4, batch_limit=1, maxiter=2,
+                   fit_hyperparameters=False, acq_batch_size=40)
+    opt = BayesianOptimizer(StubSimulator(), BOUNDS, str(tmp_path), n_initial_points=20, n_batches=1, batch_size=40,
+                            target_total=20, engine=OracleEngine(), gp_config=cfg, acquisition="qlogei", seed=2)
+    opt.optimize()
+    opt.fit_gp_model()
+    X = opt.acquire(40)
+    assert X.shape == (40, 5)
+    assert bool(((X >= 0) & (X <= 1)).all())
+
+
+def test_dropin_incremental_updates_match_refit(tmp_path):
+    """Fixed hyperparameters: later rounds fold the new rows into the factor (bordered update) with the input
+    transform frozen at the first fit; the posterior equals a fresh fit on the same transformed data."""
+    cfg = GPConfig(fit_hyperparameters=False, candidates_pool_size=256, acq_batch_size=6)
+    eng = OracleEngine()
+    opt = BayesianOptimizer(StubSimulator(), BOUNDS, str(tmp_path), n_initial_points=24, n_batches=2, batch_size=6,
+                            target_total=36, engine=eng, gp_config=cfg, seed=4)
+    opt.optimize()
+    opt.fit_gp_model()
+    assert eng.calls.get("append", 0) >= 1
+    gp = opt.gp_model
+    ref = ExactGP(gp.train_X, opt.y_tf(opt.train_Y_raw), gp.params, engine=OracleEngine()).fit()
+    Xq = opt.x_tf(torch.tensor(O.sobol_candidates(16, 5, 1)))
+    torch.testing.assert_close(gp.posterior(Xq).mean, ref.posterior(Xq).mean, rtol=1e-9, atol=1e-9)
