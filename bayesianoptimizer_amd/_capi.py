@@ -105,6 +105,15 @@ _PROTOS = {
     "gpx_fit_batched_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, c_int64, _p, c_int64, c_int64, _p,
                                       c_int64, c_int64, c_int64, _p, c_int64, c_int64, _p, c_int64, _p, c_int64,
                                       c_int64, _p, c_int64, _p, _p, c_size_t]),
+    "gpx_potrs_workspace_size": (c_int32, [c_int64, c_int64, POINTER(c_size_t)]),
+    "gpx_potrs_f64": (c_int32, [_h, c_int64, _p, c_int64, _p, _p, c_int64, c_int64, c_double, _p, _p, _p, c_size_t]),
+    "gpx_fit_factor_workspace_size": (c_int32, [c_int64, c_int64, POINTER(c_size_t)]),
+    "gpx_fit_factor_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, c_int64, _p,
+                                     c_int64, _p, _p, _p, _p, c_size_t]),
+    "gpx_fit_factor_batched_workspace_size": (c_int32, [c_int64, c_int64, c_int64, POINTER(c_size_t)]),
+    "gpx_fit_factor_batched_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, c_int64, _p, c_int64, c_int64, _p,
+                                             c_int64, c_int64, c_int64, _p, c_int64, c_int64, _p, c_int64, _p, c_int64,
+                                             _p, _p, c_size_t]),
     "gpx_append_workspace_size": (c_int32, [c_int64, c_int64, c_int64, POINTER(c_size_t)]),
     "gpx_append_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, c_int64, _p, c_int64, _p, c_int64, c_int64, _p,
                                  c_int64, _p, _p, c_int64, _p, _p, _p, c_size_t]),

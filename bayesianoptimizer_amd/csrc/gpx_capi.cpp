@@ -307,6 +307,55 @@ gpx_status gpx_fit_f64_sync(gpx_handle h, const gpx_kernel_params* p, int64_t n,
   return GPX_OK;
 }
 
+gpx_status gpx_potrs_workspace_size(int64_t n, int64_t nrhs, size_t* bytes) {
+  if (!bytes || n < 1 || nrhs < 1 || nrhs > GPX_MAX_RHS) return GPX_INVALID_ARG;
+  *bytes = gpx::potrs_workspace_bytes(padded(n), nrhs, 1) + 256;
+  return GPX_OK;
+}
+
+gpx_status gpx_potrs_f64(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv, const double* Y,
+                         int64_t ldy, int64_t nrhs, double const_mean, double* alpha, const int32_t* info, void* ws,
+                         size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_TRY(check_n(c, n));
+  if (nrhs < 1 || nrhs > GPX_MAX_RHS) return fail(c, GPX_INVALID_ARG, "nrhs must be in [1, 8]");
+  GPX_NONNULL(c, L);
+  GPX_NONNULL(c, Dinv);
+  GPX_NONNULL(c, Y);
+  GPX_NONNULL(c, alpha);
+  GPX_NONNULL(c, ws);
+  const int64_t npad = padded(n);
+  GPX_TRY(check_ld(c, ldl, npad, "L", true));
+  GPX_TRY(check_ld(c, ldy, nrhs, "Y", false));
+  size_t need = 0;
+  GPX_TRY(gpx_potrs_workspace_size(n, nrhs, &need));
+  if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "potrs workspace too small");
+  GPX_USE_DEVICE(c);
+  return hip_check(c, gpx::launch_potrs(c, (int)n, (int)npad, L, ldl, Dinv, Y, ldy, (int)nrhs, const_mean, alpha, info,
+                                        align256(ws)),
+                   "potrs");
+}
+
+gpx_status gpx_fit_factor_workspace_size(int64_t n, int64_t nrhs, size_t* bytes) {
+  return gpx_potrs_workspace_size(n, nrhs, bytes);
+}
+
+gpx_status gpx_fit_factor_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                              const double* Y, int64_t ldy, int64_t nrhs, double* K, int64_t ldk, double* Dinv,
+                              double* alpha, int32_t* info, void* ws, size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  size_t need = 0;
+  if (gpx_fit_factor_workspace_size(n, nrhs, &need) != GPX_OK)
+    return fail(c, GPX_INVALID_ARG, "invalid n / nrhs for fit");
+  if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "fit workspace too small");
+  if (!info) return fail(c, GPX_INVALID_ARG, "info is NULL");
+  GPX_TRY(gram_impl(h, p, n, X, ldx, K, ldk, info));
+  GPX_TRY(potrf_impl(h, n, K, ldk, Dinv, info, false));
+  return gpx_potrs_f64(h, n, K, ldk, Dinv, Y, ldy, nrhs, p->const_mean, alpha, info, ws, ws_bytes);
+}
+
 gpx_status gpx_append_workspace_size(int64_t n_old, int64_t n_new, int64_t nrhs, size_t* bytes) {
   if (!bytes || n_old < 1 || n_new <= n_old || nrhs < 1 || nrhs > GPX_MAX_RHS) return GPX_INVALID_ARG;
   size_t a = gpx::append_workspace_bytes(n_old, n_new), b = alpha_ws(padded(n_new), nrhs);
@@ -363,13 +412,15 @@ gpx_status gpx_fit_batched_workspace_size(int64_t n, int64_t nrhs, int64_t batch
   return GPX_OK;
 }
 
-gpx_status gpx_fit_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n, const double* X,
-                               int64_t ldx, int64_t stride_x, const double* Y, int64_t ldy, int64_t stride_y,
-                               int64_t nrhs, double* K, int64_t ldk, int64_t stride_k, double* Dinv,
-                               int64_t stride_dinv, double* W, int64_t ldw, int64_t stride_w, double* alpha,
-                               int64_t stride_alpha, int32_t* info, void* ws, size_t ws_bytes) {
+// Batched posterior updates; W == nullptr: factor + triangular solves only (gpx_fit_factor_batched_f64).
+static gpx_status fit_batched_impl(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n, const double* X,
+                                   int64_t ldx, int64_t stride_x, const double* Y, int64_t ldy, int64_t stride_y,
+                                   int64_t nrhs, double* K, int64_t ldk, int64_t stride_k, double* Dinv,
+                                   int64_t stride_dinv, double* W, int64_t ldw, int64_t stride_w, double* alpha,
+                                   int64_t stride_alpha, int32_t* info, void* ws, size_t ws_bytes) {
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return GPX_INVALID_ARG;
+  const bool inverse = W != nullptr;
   GPX_TRY(check_params(c, p));
   GPX_TRY(check_n(c, n));
   if (batch < 1 || batch > 65535) return fail(c, GPX_INVALID_ARG, "batch must be in [1, 65535]");
@@ -378,7 +429,6 @@ gpx_status gpx_fit_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t
   GPX_NONNULL(c, Y);
   GPX_NONNULL(c, K);
   GPX_NONNULL(c, Dinv);
-  GPX_NONNULL(c, W);
   GPX_NONNULL(c, alpha);
   GPX_NONNULL(c, info);
   GPX_NONNULL(c, ws);
@@ -386,17 +436,21 @@ gpx_status gpx_fit_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t
   GPX_TRY(check_ld(c, ldx, p->d, "X", false));
   GPX_TRY(check_ld(c, ldy, nrhs, "Y", false));
   GPX_TRY(check_ld(c, ldk, npad, "K", true));
-  GPX_TRY(check_ld(c, ldw, npad, "W", true));
+  if (inverse) GPX_TRY(check_ld(c, ldw, npad, "W", true));
   const int64_t nblk = npad / gpx::NB;
   if (batch > 1) {
     // problems must not overlap (a stride of 0 would make them race on the same output)
-    if (stride_x < n * ldx || stride_y < n * ldy || stride_k < npad * ldk || stride_w < npad * ldw ||
+    if (stride_x < n * ldx || stride_y < n * ldy || stride_k < npad * ldk || (inverse && stride_w < npad * ldw) ||
         stride_dinv < 2 * nblk * gpx::NB * gpx::NB || stride_alpha < npad * nrhs)
       return fail(c, GPX_INVALID_ARG, "batch strides smaller than one problem");
-    if ((stride_k | stride_w | stride_dinv) & 1) return fail(c, GPX_INVALID_ARG, "K/W/Dinv strides must be even");
+    if ((stride_k | (inverse ? stride_w : 0) | stride_dinv) & 1)
+      return fail(c, GPX_INVALID_ARG, "K/W/Dinv strides must be even");
   }
   size_t need = 0;
-  GPX_TRY(gpx_fit_batched_workspace_size(n, nrhs, batch, &need));
+  if (inverse)
+    GPX_TRY(gpx_fit_batched_workspace_size(n, nrhs, batch, &need));
+  else
+    GPX_TRY(gpx_fit_factor_batched_workspace_size(n, nrhs, batch, &need));
   if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "batched fit workspace too small");
   GPX_USE_DEVICE(c);
   gpx::Batch bt;
@@ -412,12 +466,43 @@ gpx_status gpx_fit_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t
   // the gram kernel clears info[0 .. batch) before the Cholesky (no separate memset dispatch)
   GPX_TRY(hip_check(c, gpx::launch_gram(c, *p, (int)n, (int)npad, X, ldx, K, ldk, bt, 0, info), "gram"));
   GPX_TRY(hip_check(c, gpx::launch_potrf(c, (int)npad, K, ldk, Dinv, info, bt, W, ldw), "potrf"));
+  if (!inverse)
+    return hip_check(c, gpx::launch_potrs(c, (int)n, (int)npad, K, ldk, Dinv, Y, ldy, (int)nrhs, p->const_mean, alpha,
+                                          info, slice, bt),
+                     "potrs");
   GPX_TRY(hip_check(c, gpx::launch_trtri(c, (int)npad, K, ldk, Dinv, W, ldw, slice, bt, true), "trtri"));
   double* zpart = slice;
   double* z = zpart + (size_t)(npad / 128) * npad * nrhs;
   return hip_check(c, gpx::launch_alpha(c, (int)n, (int)npad, W, ldw, Y, ldy, (int)nrhs, p->const_mean, alpha, zpart, z,
                                         bt),
                    "alpha");
+}
+
+gpx_status gpx_fit_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n, const double* X,
+                               int64_t ldx, int64_t stride_x, const double* Y, int64_t ldy, int64_t stride_y,
+                               int64_t nrhs, double* K, int64_t ldk, int64_t stride_k, double* Dinv,
+                               int64_t stride_dinv, double* W, int64_t ldw, int64_t stride_w, double* alpha,
+                               int64_t stride_alpha, int32_t* info, void* ws, size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_NONNULL(c, W);
+  return fit_batched_impl(h, p, batch, n, X, ldx, stride_x, Y, ldy, stride_y, nrhs, K, ldk, stride_k, Dinv,
+                          stride_dinv, W, ldw, stride_w, alpha, stride_alpha, info, ws, ws_bytes);
+}
+
+gpx_status gpx_fit_factor_batched_workspace_size(int64_t n, int64_t nrhs, int64_t batch, size_t* bytes) {
+  if (!bytes || n < 1 || nrhs < 1 || nrhs > GPX_MAX_RHS || batch < 1 || batch > 65535) return GPX_INVALID_ARG;
+  *bytes = gpx::potrs_workspace_bytes(padded(n), nrhs, batch) + 256;
+  return GPX_OK;
+}
+
+gpx_status gpx_fit_factor_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n,
+                                      const double* X, int64_t ldx, int64_t stride_x, const double* Y, int64_t ldy,
+                                      int64_t stride_y, int64_t nrhs, double* K, int64_t ldk, int64_t stride_k,
+                                      double* Dinv, int64_t stride_dinv, double* alpha, int64_t stride_alpha,
+                                      int32_t* info, void* ws, size_t ws_bytes) {
+  return fit_batched_impl(h, p, batch, n, X, ldx, stride_x, Y, ldy, stride_y, nrhs, K, ldk, stride_k, Dinv,
+                          stride_dinv, nullptr, 0, 0, alpha, stride_alpha, info, ws, ws_bytes);
 }
 
 gpx_status gpx_mll_workspace_size(int64_t n, size_t* bytes) {

@@ -84,6 +84,12 @@ hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, cons
 hipError_t launch_alpha(Context* c, int n, int npad, const double* W, int64_t ldw, const double* Y, int64_t ldy,
                         int nrhs, double const_mean, double* alpha, double* zpart, double* z,
                         const Batch& bt = Batch());
+// alpha from L + Dinv by forward/backward triangular solves (gpx_potrs.hip); ws: potrs_workspace_bytes, zeroed by
+// the launch itself (its hand-off granules)
+size_t potrs_workspace_bytes(int64_t npad, int64_t nrhs, int64_t batch);
+hipError_t launch_potrs(Context* c, int n, int npad, const double* L, int64_t ldl, const double* Dinv,
+                        const double* Y, int64_t ldy, int nrhs, double const_mean, double* alpha,
+                        const int32_t* info, void* ws, const Batch& bt = Batch());
 
 struct SweepBuffers {
   double* kstar;     // npad x C

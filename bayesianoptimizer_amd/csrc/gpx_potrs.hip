@@ -1,0 +1,610 @@
+// alpha = K^{-1} (Y - m) from the Cholesky factor alone (LAPACK potrs): forward L z = b, then backward L^T alpha = z,
+// in ONE persistent launch whose workgroups hand 128-row blocks of z / alpha to each other.
+// SURVEY §8a row a5 (GPyTorch's mean_cache [upstream], reached from optimization/Bayesian.py:89-94): the posterior
+// update of SURVEY §8d (Gram + Cholesky + alpha) no longer forms W = L^{-T} (n^3/3 more flops, 0.61 ms at n = 4096);
+// W is built by gpx_trtri_f64 only when a sweep, a posterior or a gradient needs it.
+//
+// Work items, in order: forward block K = 0 .. nb-1, then backward block K = nb-1 .. 0 (nb = npad / 128).  Item i
+// belongs to workgroup i mod G of its problem (G <= nb workgroups per problem, the grid sized to be co-resident), so
+// an item only ever waits on items with a smaller index, all owned by running workgroups or done.
+//   forward K:  v = b_K - sum_{J<K} L_KJ z_J, each 128x128 tile L_KJ loaded into registers BEFORE its z_J is waited
+//               for; then z_K = L_KK^{-1} v with potrf's 64-block inverses: z_a = D_a v_a, v_b -= L_ba z_a,
+//               z_b = D_b v_b.
+//   backward K: v = z_K - sum_{J>K} L_JK^T alpha_J; alpha_b = D_b^T v_b, v_a -= L_ba^T alpha_b, alpha_a = D_a^T v_a.
+// Every accumulation runs in a fixed order (J ascending forward, descending backward; fixed lane reductions), so the
+// result does not depend on timing or placement, and a batched solve equals single solves bit for bit.
+//
+// Hand-off (cdna_hip_programming.md §6 Guideline 16, form R2 — the data is the flag): every double of a published
+// block travels as two naturally aligned 8-byte {tag, 32-bit half} granules, each written by ONE agent-scope atomic
+// (sc1) store; one consumer wave re-reads the block's granules with agent-scope atomic loads until every tag equals
+// the phase's epoch (1 = z, 2 = alpha).  The granule buffer is zeroed by a memset before the launch.  Spins are
+// bounded: a solve that stops making progress sets the timeout word, every waiter then gives up and the items it
+// owned write NaN into alpha.
+#include "gpx_internal.h"
+#include "gpx_device.h"
+
+// Optional timestamp hook for tools/potrs_probe.hip (compiled out in the library).
+#ifndef GPX_POTRS_STAMP
+#define GPX_POTRS_STAMP(i)
+#endif
+
+namespace gpx {
+
+namespace {
+
+constexpr int SB = 128;       // rows per hand-off block
+constexpr int LDT = NB + 1;   // LDS row length of the 64x64 diagonal tiles
+constexpr unsigned kSpinLimit = 1u << 22;
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+// One wave: wait until all 256*NR granules of a block carry `epoch`, then write their 32-bit halves into dst
+// (SB x NR doubles, row-major; wave-private, so no workgroup barrier is needed before the wave reads it back).
+// Every wave of a consumer sweeps for itself.  The abort word is read only every 64th failed pass (its sc1 load would
+// otherwise double each poll's round trip).  Returns false on timeout / abort.
+template <int NR>
+__device__ __forceinline__ bool sweep_block(gu64* g, unsigned epoch, double* dst, gu32* abort_word) {
+  constexpr int PER = 4 * NR;  // granules per lane: SB * NR * 2 / 64
+  const int lane = threadIdx.x & 63;
+  unsigned long long x[PER];
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      x[k] = __hip_atomic_load(g + lane + 64 * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok &= (unsigned)(x[k] >> 32) == epoch;
+    }
+    if (__all(ok)) break;
+    if ((spins & 63) == 63 &&
+        (spins >= kSpinLimit || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
+      if (lane == 0) __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  unsigned* d32 = reinterpret_cast<unsigned*>(dst);
+#pragma unroll
+  for (int k = 0; k < PER; ++k) d32[lane + 64 * k] = (unsigned)x[k];  // granule gi = element gi/2, half gi%2
+  return true;
+}
+
+template <int NR>
+__device__ __forceinline__ void publish_block(gu64* g, unsigned epoch, const double* src) {
+  const unsigned* s32 = reinterpret_cast<const unsigned*>(src);
+  for (int gi = threadIdx.x; gi < SB * NR * 2; gi += WG)
+    __hip_atomic_store(g + gi, ((unsigned long long)epoch << 32) | s32[gi], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// 64x64 tile of a row-major global matrix into LDS (row length LDT)
+__device__ __forceinline__ void tile_to_lds(const double* __restrict__ G, int64_t ld, double* S) {
+  for (int e = threadIdx.x; e < NB * NB / 2; e += WG) {
+    const int r = (2 * e) >> 6, c = (2 * e) & 63;
+    const double2 v = *reinterpret_cast<const double2*>(G + (int64_t)r * ld + c);
+    S[r * LDT + c] = v.x;
+    S[r * LDT + c + 1] = v.y;
+  }
+}
+
+// out (64 x NR) = M x (TRANS: M^T x), or out -= ... (SUB); M in LDS (row length LDT), x / out in LDS (row-major,
+// NR per row).  Thread (i = t/4, q = t%4) sums j in [16q, 16q+16), the four partials are combined by lane shuffles.
+template <int NR, bool TRANS, bool SUB>
+__device__ __forceinline__ void gemv64(double* out, const double* M, const double* x) {
+  const int t = threadIdx.x, i = t >> 2, q = t & 3;
+  double p[NR];
+#pragma unroll
+  for (int rr = 0; rr < NR; ++rr) p[rr] = 0.0;
+#pragma unroll
+  for (int jj = 0; jj < 16; ++jj) {
+    const int j = 16 * q + jj;
+    const double m = TRANS ? M[j * LDT + i] : M[i * LDT + j];
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) p[rr] = fma(m, x[j * NR + rr], p[rr]);
+  }
+#pragma unroll
+  for (int rr = 0; rr < NR; ++rr) {
+    p[rr] += __shfl_xor(p[rr], 1);
+    p[rr] += __shfl_xor(p[rr], 2);
+  }
+  if (q == 0) {
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) out[i * NR + rr] = SUB ? out[i * NR + rr] - p[rr] : p[rr];
+  }
+}
+
+// NR = 8: the diagonal block is solved in three 64-steps (D_a, L_ba, D_b from LDS).
+template <int NR>
+struct SolveLds {
+  double Da[NB * LDT], Db[NB * LDT], Lba[NB * LDT];
+  double zw[WG / 64][SB * NR];  // wave-private copy of the block being consumed
+  double vs[SB * NR];           // right-hand side / working vector
+  double os[SB * NR];           // the block being produced
+};
+
+// NR = 1: the whole 128x128 inverse D_KK = L_KK^{-1} = [D_a 0; -D_b L_ba D_a  D_b] is formed at the start of the item
+// (before anything is waited for), so the step on the chain is ONE matrix-vector product.
+constexpr int LDK = SB + 4;  // LDS row length of D_KK
+struct SolveLds1 {
+  double Dk[SB * LDK];
+  double zw[WG / 64][SB];  // wave-private copy of the block being consumed
+  double vs[SB];
+};
+
+// C(64x64) = sign * A(64x64) B(64x64), operands in LDS (row lengths LDA / LDB), fp64 MFMA 16x16x4: wave w computes the
+// 32x32 quadrant (w/2, w%2).  A lower triangular (A_LOW) / B lower triangular (B_LOW) bound the k range per block.
+// Result in registers: acc[i][j][r] = C(32 (w/2) + 16 i + lane/16 + 4 r, 32 (w%2) + 16 j + lane%16).
+template <int LDA, int LDB, bool A_LOW, bool B_LOW>
+__device__ __forceinline__ void mfma64_lds(d4 (&acc)[2][2], const double* A, const double* B, double sign) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int m0 = 32 * (w >> 1), n0 = 32 * (w & 1);
+  const int l16 = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+      // k range with a non-zero product: B lower -> k >= first column of the block; A lower -> k <= last row
+      const int kb = B_LOW ? n0 + 16 * j : 0;
+      const int ke = A_LOW ? m0 + 16 * i + 16 : NB;
+      for (int k = kb; k < ke; k += 4) {
+        const double a = sign * A[(m0 + 16 * i + l16) * LDA + k + kk];
+        const double b = B[(k + kk) * LDB + n0 + 16 * j + l16];
+        acc[i][j] = mfma16x16x4(a, b, acc[i][j]);
+      }
+    }
+}
+
+template <int LDC>
+__device__ __forceinline__ void store_quadrants(double* C, const d4 (&acc)[2][2]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int m0 = 32 * (w >> 1), n0 = 32 * (w & 1);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) C[(m0 + 16 * i + (lane >> 4) + 4 * r) * LDC + n0 + 16 * j + (lane & 15)] = acc[i][j][r];
+}
+
+// D_KK of chain block K into s.Dk: D_a, D_b and L_ba staged in its blocks, T = L_ba D_a parked in the (zero) upper
+// block, then the lower-left block = -D_b T.
+__device__ __forceinline__ void form_block_inverse(SolveLds1& s, const double* __restrict__ Dinv,
+                                                   const double* __restrict__ L, int64_t ldl, int K) {
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)K * SB;
+  const double* Da = Dinv + (int64_t)(2 * K) * NB * NB;
+  const double* Db = Dinv + (int64_t)(2 * K + 1) * NB * NB;
+  const double* Lba = L + (r0 + NB) * ldl + r0;
+  for (int e = t; e < NB * NB / 2; e += WG) {
+    const int r = (2 * e) >> 6, c = (2 * e) & 63;
+    const double2 a = *reinterpret_cast<const double2*>(Da + r * NB + c);
+    const double2 b = *reinterpret_cast<const double2*>(Db + r * NB + c);
+    const double2 l = *reinterpret_cast<const double2*>(Lba + (int64_t)r * ldl + c);
+    s.Dk[r * LDK + c] = a.x;
+    s.Dk[r * LDK + c + 1] = a.y;
+    s.Dk[(NB + r) * LDK + NB + c] = b.x;
+    s.Dk[(NB + r) * LDK + NB + c + 1] = b.y;
+    s.Dk[r * LDK + NB + c] = l.x;  // L_ba parked in the upper-right block
+    s.Dk[r * LDK + NB + c + 1] = l.y;
+  }
+  __syncthreads();
+  d4 acc[2][2];
+  mfma64_lds<LDK, LDK, false, true>(acc, s.Dk + NB, s.Dk, 1.0);  // T = L_ba D_a (D_a lower)
+  __syncthreads();
+  store_quadrants<LDK>(s.Dk + NB, acc);
+  __syncthreads();
+  mfma64_lds<LDK, LDK, true, false>(acc, s.Dk + NB * LDK + NB, s.Dk + NB, -1.0);  // -D_b T (D_b lower)
+  __syncthreads();
+  store_quadrants<LDK>(s.Dk + NB * LDK, acc);
+  for (int e = t; e < NB * NB; e += WG) s.Dk[(e >> 6) * LDK + NB + (e & 63)] = 0.0;
+  __syncthreads();
+}
+
+// Off-diagonal tile of one consumed block, 64 doubles per thread.
+//  forward  (tile L_KJ, rows of block K x columns of block J): thread t owns rows rq + 32k (rq = t/8, k < 4) and the
+//           column pairs 16 c2 + 2 g (g = t%8, c2 < 8): a load instruction reads 8 x 16 B = one whole 128-B line per row;
+//  backward (tile L_JK, rows of block J x columns of block K): thread t owns column t/2 of block K and rows
+//           64 (t%2) .. +63 of block J (two 256-B runs per instruction).
+struct TileRegs {
+  double2 v[32];
+};
+
+__device__ __forceinline__ void load_tile_fwd(TileRegs& R, const double* __restrict__ L, int64_t ldl, int64_t r0,
+                                              int64_t c0) {
+  const int t = threadIdx.x, g = t & 7, rq = t >> 3;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int c2 = 0; c2 < 8; ++c2)
+      R.v[8 * k + c2] = *reinterpret_cast<const double2*>(L + (r0 + rq + 32 * k) * ldl + c0 + 16 * c2 + 2 * g);
+}
+
+__device__ __forceinline__ void load_tile_bwd(TileRegs& R, const double* __restrict__ L, int64_t ldl, int64_t r0,
+                                              int64_t c0) {
+  const int t = threadIdx.x, c = t >> 1, h = t & 1;
+  const double* src = L + (r0 + NB * h) * ldl + c0 + c;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) R.v[i] = make_double2(src[(int64_t)(2 * i) * ldl], src[(int64_t)(2 * i + 1) * ldl]);
+}
+
+template <int NR>
+__device__ __forceinline__ void fma_fwd(double (&acc)[4][NR], const TileRegs& R, const double* z) {
+  const int g = threadIdx.x & 7;
+  if constexpr (NR == 1) {
+    // the thread's 16 z entries as 8 16-byte LDS reads issued back to back, then the FMAs
+    double2 zz[8];
+#pragma unroll
+    for (int c2 = 0; c2 < 8; ++c2) zz[c2] = *reinterpret_cast<const double2*>(z + 16 * c2 + 2 * g);
+#pragma unroll
+    for (int c2 = 0; c2 < 8; ++c2)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        acc[k][0] = fma(R.v[8 * k + c2].y, zz[c2].y, fma(R.v[8 * k + c2].x, zz[c2].x, acc[k][0]));
+    return;
+  }
+#pragma unroll
+  for (int c2 = 0; c2 < 8; ++c2) {
+    const int c = 16 * c2 + 2 * g;
+    double z0[NR], z1[NR];
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+      z0[rr] = z[c * NR + rr];
+      z1[rr] = z[(c + 1) * NR + rr];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int rr = 0; rr < NR; ++rr)
+        acc[k][rr] = fma(R.v[8 * k + c2].y, z1[rr], fma(R.v[8 * k + c2].x, z0[rr], acc[k][rr]));
+  }
+}
+
+template <int NR>
+__device__ __forceinline__ void fma_bwd(double (&acc)[4][NR], const TileRegs& R, const double* a) {
+  const int h = threadIdx.x & 1;
+  if constexpr (NR == 1) {
+    // the 64 alpha entries of this half as 16-byte LDS reads (same address across the lanes of a half: broadcast),
+    // two independent accumulation chains
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int i0 = 0; i0 < 32; i0 += 8) {
+      double2 aa[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) aa[i] = *reinterpret_cast<const double2*>(a + NB * h + 2 * (i0 + i));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        s0 = fma(R.v[i0 + i].x, aa[i].x, s0);
+        s1 = fma(R.v[i0 + i].y, aa[i].y, s1);
+      }
+    }
+    acc[0][0] += s0 + s1;
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 32; ++i)
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr)
+      acc[0][rr] = fma(R.v[i].y, a[(NB * h + 2 * i + 1) * NR + rr], fma(R.v[i].x, a[(NB * h + 2 * i) * NR + rr],
+                                                                          acc[0][rr]));
+}
+
+}  // namespace
+
+// Single right-hand side: D_KK formed up front, one product on the chain, the block published from registers.
+__device__ void potrs_items_1(int n, int npad, const double* __restrict__ L, int64_t ldl,
+                              const double* __restrict__ Dinv, const double* __restrict__ Y, int64_t ldy,
+                              double const_mean, double* __restrict__ alpha, gu64* gz, gu64* ga, gu32* abort_word,
+                              SolveLds1& s, int& s_abort) {
+  const int t = threadIdx.x, w = t >> 6;
+  const int nb = npad / SB;
+  const int G = gridDim.x;
+  for (int item = blockIdx.x; item < 2 * nb; item += G) {
+    const bool fwd = item < nb;
+    const int K = fwd ? item : 2 * nb - 1 - item;
+    const int64_t r0 = (int64_t)K * SB;
+    const int jcount = fwd ? K : nb - 1 - K;
+    GPX_POTRS_STAMP(0);
+    auto jblk = [&](int jj) { return fwd ? jj : nb - 1 - jj; };
+    TileRegs ta, tb;
+    auto load_tile = [&](TileRegs& R, int jj) {
+      if (fwd)
+        load_tile_fwd(R, L, ldl, r0, (int64_t)jblk(jj) * SB);
+      else
+        load_tile_bwd(R, L, ldl, (int64_t)jblk(jj) * SB, r0);
+    };
+    if (jcount > 0) load_tile(ta, 0);  // in flight while D_KK is formed
+    form_block_inverse(s, Dinv, L, ldl, K);
+    if (fwd) {
+      if (t < SB) s.vs[t] = (r0 + t < n) ? Y[(r0 + t) * ldy] - const_mean : 0.0;
+    } else if (w == 0) {
+      if (!sweep_block<1>(gz + r0 * 2, 1u, s.vs, abort_word) && (t & 63) == 0) s_abort = 1;
+    }
+    double acc[4][1];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k][0] = 0.0;
+    // every wave polls the block it needs into its own LDS copy (no workgroup barrier in the loop)
+    double* zw = s.zw[w];
+    auto consume = [&](const TileRegs& R, int jj) {
+      if (!sweep_block<1>((fwd ? gz : ga) + (int64_t)jblk(jj) * SB * 2, fwd ? 1u : 2u, zw, abort_word) &&
+          (t & 63) == 0)
+        s_abort = 1;
+      GPX_POTRS_STAMP(1);
+      if (fwd)
+        fma_fwd<1>(acc, R, zw);
+      else
+        fma_bwd<1>(acc, R, zw);
+    };
+    // no workgroup barrier in this loop; the next tile is loaded while the current one's block is waited for
+    for (int jj = 0; jj < jcount; jj += 2) {
+      const bool two = jj + 1 < jcount;
+      if (two) load_tile(tb, jj + 1);
+      consume(ta, jj);
+      if (!two) break;
+      if (jj + 2 < jcount) load_tile(ta, jj + 2);
+      consume(tb, jj + 1);
+    }
+    // v = b - sum (right-hand side in s.vs), one barrier, then z = D_KK v (forward) / alpha = D_KK^T v (backward)
+    if (fwd) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc[k][0] += __shfl_xor(acc[k][0], 1);
+        acc[k][0] += __shfl_xor(acc[k][0], 2);
+        acc[k][0] += __shfl_xor(acc[k][0], 4);
+      }
+    } else {
+      acc[0][0] += __shfl_xor(acc[0][0], 1);
+    }
+    __syncthreads();  // s.vs (right-hand side) complete
+    if (fwd) {
+      if ((t & 7) == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s.vs[(t >> 3) + 32 * k] -= acc[k][0];
+      }
+    } else if ((t & 1) == 0) {
+      s.vs[t >> 1] -= acc[0][0];
+    }
+    __syncthreads();
+    GPX_POTRS_STAMP(2);
+    const bool aborted = s_abort != 0;  // uniform; sticky for the rest of the launch
+    if (fwd) {
+      const int g = t & 7, rq = t >> 3;
+      // LDS reads batched ahead of the FMAs (8 x 16 B per row, the thread's 16 v entries once)
+      double2 vv[8];
+#pragma unroll
+      for (int c2 = 0; c2 < 8; ++c2) vv[c2] = *reinterpret_cast<const double2*>(s.vs + 16 * c2 + 2 * g);
+      double z[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        double2 d[8];
+#pragma unroll
+        for (int c2 = 0; c2 < 8; ++c2)
+          d[c2] = *reinterpret_cast<const double2*>(s.Dk + (rq + 32 * k) * LDK + 16 * c2 + 2 * g);
+        double z0 = 0.0, z1 = 0.0;
+#pragma unroll
+        for (int c2 = 0; c2 < 8; ++c2) {
+          z0 = fma(d[c2].x, vv[c2].x, z0);
+          z1 = fma(d[c2].y, vv[c2].y, z1);
+        }
+        z[k] = z0 + z1;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        z[k] += __shfl_xor(z[k], 1);
+        z[k] += __shfl_xor(z[k], 2);
+        z[k] += __shfl_xor(z[k], 4);
+        if (aborted) z[k] = __builtin_nan("");
+      }
+      GPX_POTRS_STAMP(3);
+      if (g < 2) {  // lanes 0 / 1 of a row publish its low / high half
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const unsigned long long u = __double_as_longlong(z[k]);
+          __hip_atomic_store(gz + (r0 + rq + 32 * k) * 2 + g, (1ull << 32) | (g ? (u >> 32) : (u & 0xffffffffull)),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    } else {
+      const int c = t >> 1, h = t & 1;
+      double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+      for (int i0 = 0; i0 < NB; i0 += 16) {
+        double dd[16];
+        double2 vv[8];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dd[i] = s.Dk[(NB * h + i0 + i) * LDK + c];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) vv[i] = *reinterpret_cast<const double2*>(s.vs + NB * h + i0 + 2 * i);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          a0 = fma(dd[2 * i], vv[i].x, a0);
+          a1 = fma(dd[2 * i + 1], vv[i].y, a1);
+        }
+      }
+      double a = a0 + a1;
+      a += __shfl_xor(a, 1);
+      if (aborted) a = __builtin_nan("");
+      GPX_POTRS_STAMP(3);
+      const unsigned long long u = __double_as_longlong(a);
+      __hip_atomic_store(ga + (r0 + c) * 2 + h, (2ull << 32) | (h ? (u >> 32) : (u & 0xffffffffull)),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (h == 0) alpha[r0 + c] = (r0 + c < n || aborted) ? a : 0.0;
+    }
+    __syncthreads();  // LDS reuse by the next item
+  }
+}
+
+template <int NR>
+__device__ void potrs_items(int n, int npad, const double* __restrict__ L, int64_t ldl, const double* __restrict__ Dinv,
+                            const double* __restrict__ Y, int64_t ldy, int nrhs, double const_mean,
+                            double* __restrict__ alpha, gu64* gz, gu64* ga, gu32* abort_word, SolveLds<NR>& s,
+                            int& s_abort) {
+  const int t = threadIdx.x, w = t >> 6;
+  double* zw = s.zw[w];
+  const int nb = npad / SB;
+  const int G = gridDim.x;
+  for (int item = blockIdx.x; item < 2 * nb; item += G) {
+    const bool fwd = item < nb;
+    const int K = fwd ? item : 2 * nb - 1 - item;
+    const int64_t r0 = (int64_t)K * SB;
+    const int jcount = fwd ? K : nb - 1 - K;
+    auto jblk = [&](int jj) { return fwd ? jj : nb - 1 - jj; };
+    TileRegs ta;
+    auto load_tile = [&](TileRegs& R, int jj) {
+      if (fwd)
+        load_tile_fwd(R, L, ldl, r0, (int64_t)jblk(jj) * SB);
+      else
+        load_tile_bwd(R, L, ldl, (int64_t)jblk(jj) * SB, r0);
+    };
+    if (jcount > 0) load_tile(ta, 0);
+    // diagonal 128-block: D_a, D_b (potrf's inverses of the 64-blocks) and L_ba
+    tile_to_lds(Dinv + (int64_t)(2 * K) * NB * NB, NB, s.Da);
+    tile_to_lds(Dinv + (int64_t)(2 * K + 1) * NB * NB, NB, s.Db);
+    tile_to_lds(L + (r0 + NB) * ldl + r0, ldl, s.Lba);
+    if (fwd) {
+      for (int e = t; e < SB * NR; e += WG) {
+        const int row = e / NR, rr = e % NR;
+        const int64_t gi = r0 + row;
+        s.vs[e] = (rr < nrhs && gi < n) ? Y[gi * ldy + rr] - const_mean : 0.0;
+      }
+    } else if (w == 0) {
+      if (!sweep_block<NR>(gz + r0 * NR * 2, 1u, s.vs, abort_word) && (t & 63) == 0) s_abort = 1;
+    }
+    double acc[4][NR];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int rr = 0; rr < NR; ++rr) acc[k][rr] = 0.0;
+    // one register tile (the sweep's 4 NR granules per lane and 4 NR accumulators leave no room for a second one)
+    for (int jj = 0; jj < jcount; ++jj) {
+      if (jj > 0) load_tile(ta, jj);
+      if (!sweep_block<NR>((fwd ? gz : ga) + (int64_t)jblk(jj) * SB * NR * 2, fwd ? 1u : 2u, zw, abort_word) &&
+          (t & 63) == 0)
+        s_abort = 1;
+      if (fwd)
+        fma_fwd<NR>(acc, ta, zw);
+      else
+        fma_bwd<NR>(acc, ta, zw);
+    }
+    __syncthreads();  // staged diagonal block, right-hand side and the abort flag of every wave's sweeps
+    const bool aborted = s_abort != 0;
+    if (fwd) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) {
+          acc[k][rr] += __shfl_xor(acc[k][rr], 1);
+          acc[k][rr] += __shfl_xor(acc[k][rr], 2);
+          acc[k][rr] += __shfl_xor(acc[k][rr], 4);
+        }
+      if ((t & 7) == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int rr = 0; rr < NR; ++rr) s.vs[((t >> 3) + 32 * k) * NR + rr] -= acc[k][rr];
+      }
+    } else {
+#pragma unroll
+      for (int rr = 0; rr < NR; ++rr) acc[0][rr] += __shfl_xor(acc[0][rr], 1);
+      if ((t & 1) == 0) {
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) s.vs[(t >> 1) * NR + rr] -= acc[0][rr];
+      }
+    }
+    __syncthreads();
+    if (fwd) {
+      gemv64<NR, false, false>(s.os, s.Da, s.vs);
+      __syncthreads();
+      gemv64<NR, false, true>(s.vs + NB * NR, s.Lba, s.os);
+      __syncthreads();
+      gemv64<NR, false, false>(s.os + NB * NR, s.Db, s.vs + NB * NR);
+    } else {
+      gemv64<NR, true, false>(s.os + NB * NR, s.Db, s.vs + NB * NR);
+      __syncthreads();
+      gemv64<NR, true, true>(s.vs, s.Lba, s.os + NB * NR);
+      __syncthreads();
+      gemv64<NR, true, false>(s.os, s.Da, s.vs);
+    }
+    __syncthreads();
+    if (aborted) {
+      for (int e = t; e < SB * NR; e += WG) s.os[e] = __builtin_nan("");
+      __syncthreads();
+    }
+    publish_block<NR>((fwd ? gz : ga) + r0 * NR * 2, fwd ? 1u : 2u, s.os);
+    if (!fwd) {
+      for (int e = t; e < SB * nrhs; e += WG) {
+        const int row = e / nrhs, rr = e % nrhs;
+        alpha[(r0 + row) * nrhs + rr] = (r0 + row < n || aborted) ? s.os[row * NR + rr] : 0.0;
+      }
+    }
+    __syncthreads();  // LDS reuse by the next item
+  }
+}
+
+template <int NR>
+__global__ void __launch_bounds__(WG) potrs_kernel(int n, int npad, const double* __restrict__ L, int64_t ldl,
+                                                   const double* __restrict__ Dinv, const double* __restrict__ Y,
+                                                   int64_t ldy, int nrhs, double const_mean, double* __restrict__ alpha,
+                                                   const int32_t* __restrict__ info, unsigned long long* granules,
+                                                   unsigned* abort_ptr, int64_t sl, int64_t sd, int64_t sy, int64_t sa,
+                                                   int64_t sg) {
+  const int prob = blockIdx.y;
+  L += prob * sl;
+  Dinv += prob * sd;
+  Y += prob * sy;
+  alpha += prob * sa;
+  gu64* gz = (gu64*)(granules + prob * sg);  // forward blocks (epoch 1)
+  gu64* ga = gz + (int64_t)npad * NR * 2;     // backward blocks (epoch 2)
+  gu32* abort_word = (gu32*)(abort_ptr + prob);
+  if (info && info[prob] != 0) return;  // failed factor: nothing to solve (uniform over the problem's workgroups)
+  __shared__ int s_abort;
+  if (threadIdx.x == 0) s_abort = 0;
+  if constexpr (NR == 1) {
+    __shared__ __attribute__((aligned(16))) SolveLds1 s;
+    __syncthreads();
+    potrs_items_1(n, npad, L, ldl, Dinv, Y, ldy, const_mean, alpha, gz, ga, abort_word, s, s_abort);
+  } else {
+    __shared__ __attribute__((aligned(16))) SolveLds<NR> s;
+    __syncthreads();
+    potrs_items<NR>(n, npad, L, ldl, Dinv, Y, ldy, nrhs, const_mean, alpha, gz, ga, abort_word, s, s_abort);
+  }
+}
+
+size_t potrs_granule_bytes(int64_t npad, int64_t nrhs) {
+  const int64_t nr = nrhs == 1 ? 1 : GPX_MAX_RHS;
+  return (size_t)(2 * npad * nr * 2) * sizeof(unsigned long long);
+}
+
+hipError_t launch_potrs(Context* c, int n, int npad, const double* L, int64_t ldl, const double* Dinv,
+                        const double* Y, int64_t ldy, int nrhs, double const_mean, double* alpha,
+                        const int32_t* info, void* ws, const Batch& bt) {
+  LaunchTimer tm(c, GPX_TIMER_ALPHA);
+  const int nb = npad / SB;
+  // granules of every problem, then one abort word per problem; zeroed as ONE block from the workspace start
+  const size_t gbytes = potrs_granule_bytes(npad, nrhs);
+  auto* granules = reinterpret_cast<unsigned long long*>(ws);
+  auto* abort_word = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(ws) + gbytes * bt.count);
+  const size_t clear = ((gbytes * bt.count + 4 * (size_t)bt.count) + 15) & ~(size_t)15;
+  hipError_t e = hipMemsetAsync(ws, 0, clear, c->stream);
+  if (e != hipSuccess) return e;
+  // co-resident grid (one 124 KB workgroup per CU at NR = 8): at most 256 workgroups in all
+  int G = 256 / bt.count;
+  if (G < 1) G = 1;
+  if (G > nb) G = nb;
+  const int64_t sg = (int64_t)(gbytes / sizeof(unsigned long long));
+  if (nrhs == 1)
+    potrs_kernel<1><<<dim3(G, bt.count), WG, 0, c->stream>>>(n, npad, L, ldl, Dinv, Y, ldy, nrhs, const_mean, alpha,
+                                                             info, granules, abort_word, bt.k, bt.dinv, bt.y,
+                                                             bt.alpha, sg);
+  else
+    potrs_kernel<GPX_MAX_RHS><<<dim3(G, bt.count), WG, 0, c->stream>>>(n, npad, L, ldl, Dinv, Y, ldy, nrhs,
+                                                                       const_mean, alpha, info, granules, abort_word,
+                                                                       bt.k, bt.dinv, bt.y, bt.alpha, sg);
+  return hipGetLastError();
+}
+
+size_t potrs_workspace_bytes(int64_t npad, int64_t nrhs, int64_t batch) {
+  return potrs_granule_bytes(npad, nrhs) * batch + 4 * batch + 64;
+}
+
+}  // namespace gpx

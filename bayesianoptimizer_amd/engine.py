@@ -102,7 +102,8 @@ class GPState:
     L: padded lower Cholesky factor (only its lower triangle is defined), W = L^{-T} (upper), alpha =
     K^{-1}(Y - m) (padded_n x nrhs), Dinv: inverses of the 64x64 diagonal blocks of L.  L and W may be
     npad x npad views of larger capacity x capacity buffers (``GPEngine.append`` grows into them); their
-    leading dimension is ``L.stride(0)``.
+    leading dimension is ``L.stride(0)``.  ``W_ready`` is False after a factor-only update (``GPEngine.fit`` with
+    ``inverse=False``): W is then built by ``GPEngine.inverse`` the first time a sweep / posterior / gradient needs it.
     """
 
     X: torch.Tensor
@@ -116,6 +117,7 @@ class GPState:
     npad: int
     nrhs: int
     _batch: Optional[tuple] = field(default=None, repr=False)  # stacked tensors of a fit_batched call
+    W_ready: bool = True
 
     @property
     def d(self) -> int:
@@ -208,12 +210,15 @@ class GPEngine:
             params=params, n=n, npad=npad, nrhs=nrhs)
 
     def fit(self, X, Y, params: KernelParams, check: bool = True, out: Optional[GPState] = None,
-            capacity: int = 0) -> GPState:
-        """One posterior update: Gram + blocked Cholesky + L^{-T} + alpha for up to 8 outputs sharing X.
+            capacity: int = 0, inverse: bool = False) -> GPState:
+        """One posterior update: Gram + blocked Cholesky + alpha for up to 8 outputs sharing X.
 
-        With ``check`` (default) synchronises and raises NotPositiveDefiniteError like psd_safe_cholesky
-        would; with ``check=False`` stays asynchronous (inspect ``state.info`` later).  ``capacity``: training
-        points to reserve buffer room for (later ``append`` calls grow in place up to it).
+        ``inverse=False`` (default): alpha by the triangular solves of gpx_fit_factor_f64 and W = L^{-T} left to
+        ``GPEngine.inverse``, which the sweep / posterior / gradient / append entry points call on first use (an
+        update followed by another update before any sweep never pays for W).  ``inverse=True``: gpx_fit_f64 (W formed
+        in the same call, alpha from W).  With ``check`` (default) synchronises and raises NotPositiveDefiniteError like
+        psd_safe_cholesky would; with ``check=False`` stays asynchronous (inspect ``state.info`` later).  ``capacity``:
+        training points to reserve buffer room for (later ``append`` calls grow in place up to it).
         """
         X = self._as_f64(X, "X")
         Y = self._as_f64(Y, "Y")
@@ -228,18 +233,56 @@ class GPEngine:
             self.alloc_state(X, nrhs, params, capacity)
         st.X, st.params = X, params
         nbytes = ctypes.c_size_t()
-        self._check(self.lib.gpx_fit_workspace_size(n, nrhs, ctypes.byref(nbytes)))
-        ws = self.workspace("fit", nbytes.value)
         self._bind_stream()
-        self._check(self.lib.gpx_fit_f64(
-            self.handle, ctypes.byref(pc), n, _ptr(X), X.stride(0), _ptr(Y), Y.stride(0), nrhs,
-            _ptr(st.L), st.L.stride(0), _ptr(st.Dinv), _ptr(st.W), st.W.stride(0), _ptr(st.alpha), _ptr(st.info),
-            _ptr(ws), ws.numel()))
+        if inverse:
+            self._check(self.lib.gpx_fit_workspace_size(n, nrhs, ctypes.byref(nbytes)))
+            ws = self.workspace("fit", nbytes.value)
+            self._check(self.lib.gpx_fit_f64(
+                self.handle, ctypes.byref(pc), n, _ptr(X), X.stride(0), _ptr(Y), Y.stride(0), nrhs,
+                _ptr(st.L), st.L.stride(0), _ptr(st.Dinv), _ptr(st.W), st.W.stride(0), _ptr(st.alpha), _ptr(st.info),
+                _ptr(ws), ws.numel()))
+        else:
+            self._check(self.lib.gpx_fit_factor_workspace_size(n, nrhs, ctypes.byref(nbytes)))
+            ws = self.workspace("potrs", nbytes.value)
+            self._check(self.lib.gpx_fit_factor_f64(
+                self.handle, ctypes.byref(pc), n, _ptr(X), X.stride(0), _ptr(Y), Y.stride(0), nrhs,
+                _ptr(st.L), st.L.stride(0), _ptr(st.Dinv), _ptr(st.alpha), _ptr(st.info), _ptr(ws), ws.numel()))
+        st.W_ready = inverse
         if check:
             piv = st.pivot_failure()
             if piv >= 0:
                 raise NotPositiveDefiniteError(piv)
         return st
+
+    def inverse(self, state: GPState) -> GPState:
+        """Build W = L^{-T} of a factor-only update (gpx_trtri_f64 from L and the diagonal-block inverses); no-op when
+        it is already there.  Asynchronous."""
+        if state.W_ready:
+            return state
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_trtri_workspace_size(state.n, ctypes.byref(nbytes)))
+        ws = self.workspace("fit", nbytes.value)
+        self._bind_stream()
+        self._check(self.lib.gpx_trtri_f64(self.handle, state.n, _ptr(state.L), state.L.stride(0), _ptr(state.Dinv),
+                                           _ptr(state.W), state.W.stride(0), _ptr(ws), ws.numel()))
+        state.W_ready = True
+        return state
+
+    def potrs(self, state: GPState, Y) -> torch.Tensor:
+        """alpha = K^{-1}(Y - const_mean) from the state's factor alone (gpx_potrs_f64): new targets on the same X."""
+        Y = self._as_f64(Y, "Y")
+        if Y.shape[0] != state.n:
+            raise ValueError(f"Y must have {state.n} rows, got {Y.shape[0]}")
+        nrhs = Y.shape[1]
+        alpha = torch.empty((state.npad, nrhs), dtype=torch.float64, device=self.device)
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_potrs_workspace_size(state.n, nrhs, ctypes.byref(nbytes)))
+        ws = self.workspace("potrs", nbytes.value)
+        self._bind_stream()
+        self._check(self.lib.gpx_potrs_f64(
+            self.handle, state.n, _ptr(state.L), state.L.stride(0), _ptr(state.Dinv), _ptr(Y), Y.stride(0), nrhs,
+            float(state.params.const_mean), _ptr(alpha), _ptr(state.info), _ptr(ws), ws.numel()))
+        return alpha
 
     def append(self, state: GPState, X, Y, check: bool = True, growth: float = 1.5) -> GPState:
         """Incremental posterior update: X / Y hold ALL training rows, the first ``state.n`` of them
@@ -258,6 +301,7 @@ class GPEngine:
             raise ValueError(f"Y must have shape ({n_new}, {state.nrhs}), got {tuple(Y.shape)}")
         if n_new <= n_old:
             raise ValueError(f"append needs more rows than the fitted {n_old}, got {n_new}")
+        self.inverse(state)  # the bordered update extends W
         npad = self.padded_n(n_new)
         ld = state.L.stride(0)
         if npad > ld or state.Dinv.shape[0] < 2 * (npad // 64) or state.W.stride(0) != ld:
@@ -291,11 +335,12 @@ class GPEngine:
         return state
 
     def fit_batched(self, X, Y, params: KernelParams, check: bool = True,
-                    out: Optional[Sequence[GPState]] = None) -> list:
+                    out: Optional[Sequence[GPState]] = None, inverse: bool = False) -> list:
         """Posterior updates of B independent problems (X: B x n x d, Y: B x n or B x n x nrhs) sharing n, d and the
-        hyperparameters (restarts / seeds, BASELINE configs[3]) in the same launches (gpx_fit_batched_f64).  Returns
-        one GPState per problem (views into stacked device tensors); results equal B calls of ``fit``.  With
-        ``check`` synchronises and raises NotPositiveDefiniteError for the first failing problem."""
+        hyperparameters (restarts / seeds, BASELINE configs[3]) in the same launches (gpx_fit_factor_batched_f64, or
+        gpx_fit_batched_f64 with ``inverse``: W formed for every problem in the same launches).  Returns one GPState per
+        problem (views into stacked device tensors); results equal B calls of ``fit``.  With ``check`` synchronises and
+        raises NotPositiveDefiniteError for the first failing problem."""
         X = X if isinstance(X, torch.Tensor) else torch.as_tensor(X)
         Y = Y if isinstance(Y, torch.Tensor) else torch.as_tensor(Y)
         X = X.to(device=self.device, dtype=torch.float64).contiguous()
@@ -325,17 +370,25 @@ class GPEngine:
             Ab = torch.empty((B, npad, nrhs), dtype=torch.float64, device=dev)
             Ib = torch.zeros((B,), dtype=torch.int32, device=dev)
         nbytes = ctypes.c_size_t()
-        self._check(self.lib.gpx_fit_batched_workspace_size(n, nrhs, B, ctypes.byref(nbytes)))
-        ws = self.workspace("fit_batched", nbytes.value)
         self._bind_stream()
-        self._check(self.lib.gpx_fit_batched_f64(
-            self.handle, ctypes.byref(pc), B, n, _ptr(X), X.stride(1), X.stride(0), _ptr(Y), Y.stride(1), Y.stride(0),
-            nrhs, _ptr(Lb), npad, Lb.stride(0), _ptr(Db), Db.stride(0), _ptr(Wb), npad, Wb.stride(0), _ptr(Ab),
-            Ab.stride(0), _ptr(Ib), _ptr(ws), ws.numel()))
+        if inverse:
+            self._check(self.lib.gpx_fit_batched_workspace_size(n, nrhs, B, ctypes.byref(nbytes)))
+            ws = self.workspace("fit_batched", nbytes.value)
+            self._check(self.lib.gpx_fit_batched_f64(
+                self.handle, ctypes.byref(pc), B, n, _ptr(X), X.stride(1), X.stride(0), _ptr(Y), Y.stride(1),
+                Y.stride(0), nrhs, _ptr(Lb), npad, Lb.stride(0), _ptr(Db), Db.stride(0), _ptr(Wb), npad, Wb.stride(0),
+                _ptr(Ab), Ab.stride(0), _ptr(Ib), _ptr(ws), ws.numel()))
+        else:
+            self._check(self.lib.gpx_fit_factor_batched_workspace_size(n, nrhs, B, ctypes.byref(nbytes)))
+            ws = self.workspace("potrs_batched", nbytes.value)
+            self._check(self.lib.gpx_fit_factor_batched_f64(
+                self.handle, ctypes.byref(pc), B, n, _ptr(X), X.stride(1), X.stride(0), _ptr(Y), Y.stride(1),
+                Y.stride(0), nrhs, _ptr(Lb), npad, Lb.stride(0), _ptr(Db), Db.stride(0), _ptr(Ab), Ab.stride(0),
+                _ptr(Ib), _ptr(ws), ws.numel()))
         states = []
         for b in range(B):
             states.append(GPState(X=X[b], L=Lb[b], W=Wb[b], Dinv=Db[b], alpha=Ab[b], info=Ib[b:b + 1], params=params,
-                                  n=n, npad=npad, nrhs=nrhs, _batch=(Lb, Wb, Db, Ab, Ib)))
+                                  n=n, npad=npad, nrhs=nrhs, _batch=(Lb, Wb, Db, Ab, Ib), W_ready=inverse))
         if check:
             bad = Ib.cpu().numpy()
             for b in range(B):
@@ -383,6 +436,7 @@ class GPEngine:
         if Xs.shape[1] != state.d:
             raise ValueError(f"Xs has {Xs.shape[1]} columns, model has d={state.d}")
         m = Xs.shape[0]
+        self.inverse(state)
         mean = torch.empty((m, state.nrhs), dtype=torch.float64, device=self.device)
         var = torch.empty((m,), dtype=torch.float64, device=self.device)
         if m == 0:
@@ -410,6 +464,7 @@ class GPEngine:
         m = Xs.shape[0]
         if m == 0:
             raise ValueError("empty candidate set")
+        self.inverse(state)
         kid = ACQ_KINDS[kind.lower()] if isinstance(kind, str) else int(kind)
         if alpha is None:
             alpha = state.alpha[:, 0]
@@ -446,6 +501,7 @@ class GPEngine:
             raise ValueError(f"Xs has {d} columns, model has d={state.d}")
         if m % q:
             raise ValueError(f"{m} candidates do not form q-batches of {q}")
+        self.inverse(state)
         if alpha is None:
             alpha = state.alpha[:, 0]
         alpha = alpha.to(device=self.device, dtype=torch.float64).contiguous()
@@ -487,6 +543,7 @@ class GPEngine:
             raise ValueError(f"Y must have shape ({state.n}, {state.nrhs}), got {tuple(Y.shape)}")
         if out is None:
             out = torch.empty((_capi.MLL_NOUT,), dtype=torch.float64, device=self.device)
+        self.inverse(state)
         nbytes = ctypes.c_size_t()
         self._check(self.lib.gpx_mll_workspace_size(state.n, ctypes.byref(nbytes)))
         ws = self.workspace("mll", nbytes.value)

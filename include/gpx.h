@@ -163,6 +163,26 @@ gpx_status gpx_fit_f64_sync(gpx_handle h, const gpx_kernel_params* p, int64_t n,
                             double* W, int64_t ldw, double* alpha, int32_t* info, void* ws, size_t ws_bytes,
                             int32_t* info_host);
 
+/* alpha = K^{-1} (Y - const_mean) from the factor alone (LAPACK potrs): forward L z = Y - m, backward L^T alpha = z,
+ * with L and Dinv as gpx_potrf_f64 left them (no W needed).  Y: n x nrhs (leading dim ldy), alpha: contiguous
+ * padded_n x nrhs (rows >= n are 0).  info (device, nullable): the factor's pivot word — a failed factor (non-zero)
+ * leaves alpha untouched.  One launch; its workgroups hand 128-row blocks of z / alpha to each other inside it
+ * (deterministic: fixed accumulation order).  Replaces the ExactGP mean_cache [upstream]. */
+gpx_status gpx_potrs_workspace_size(int64_t n, int64_t nrhs, size_t* bytes);
+gpx_status gpx_potrs_f64(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv, const double* Y,
+                         int64_t ldy, int64_t nrhs, double const_mean, double* alpha, const int32_t* info, void* ws,
+                         size_t ws_bytes);
+
+/* The posterior update as SURVEY §8d defines it — Gram + Cholesky + alpha — WITHOUT the explicit inverse: alpha by
+ * gpx_potrs_f64.  K (padded, in/out: holds L afterwards), Dinv, alpha, info as in gpx_fit_f64.  Everything the fit
+ * caches for prediction is then ready except W = L^{-T}, which gpx_trtri_f64(L, Dinv) builds when a sweep, a posterior,
+ * an MLL gradient or an append needs it (the inverse costs as much as the factorisation; an update that is followed
+ * by more updates before the next sweep never pays it). */
+gpx_status gpx_fit_factor_workspace_size(int64_t n, int64_t nrhs, size_t* bytes);
+gpx_status gpx_fit_factor_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
+                              const double* Y, int64_t ldy, int64_t nrhs, double* K, int64_t ldk, double* Dinv,
+                              double* alpha, int32_t* info, void* ws, size_t ws_bytes);
+
 /* Batched posterior updates: `batch` independent problems of the same n, d and kernel parameters (restarts /
  * seeds: BASELINE configs[3], the per-batch `info` of the SURVEY §8b proposal) in the SAME launches, the problem
  * index being one more grid dimension.  Every array of problem b starts at base + b * stride_* (element strides,
@@ -175,6 +195,13 @@ gpx_status gpx_fit_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t
                                int64_t nrhs, double* K, int64_t ldk, int64_t stride_k, double* Dinv,
                                int64_t stride_dinv, double* W, int64_t ldw, int64_t stride_w, double* alpha,
                                int64_t stride_alpha, int32_t* info, void* ws, size_t ws_bytes);
+/* The same without W (gpx_fit_factor_f64 per problem, bit-identical to it). */
+gpx_status gpx_fit_factor_batched_workspace_size(int64_t n, int64_t nrhs, int64_t batch, size_t* bytes);
+gpx_status gpx_fit_factor_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n,
+                                      const double* X, int64_t ldx, int64_t stride_x, const double* Y, int64_t ldy,
+                                      int64_t stride_y, int64_t nrhs, double* K, int64_t ldk, int64_t stride_k,
+                                      double* Dinv, int64_t stride_dinv, double* alpha, int64_t stride_alpha,
+                                      int32_t* info, void* ws, size_t ws_bytes);
 
 /* Incremental posterior update: rows n_old .. n_new-1 of X / Y appended to a GP whose L, Dinv and W
  * hold a successful fit (gpx_fit_f64 or an earlier append) of the first n_old rows with the SAME kernel parameters.

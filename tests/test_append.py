@@ -21,6 +21,8 @@ def _problem(n, d, nrhs, seed):
 
 
 def _compare_states(engine, st, ref, n, atol_scale=1e-9):
+    engine.inverse(st)
+    engine.inverse(ref)
     Lg = torch.tril(st.L[:n, :n]).cpu().numpy()
     Lr = torch.tril(ref.L[:n, :n]).cpu().numpy()
     assert np.abs(Lg - Lr).max() <= atol_scale * np.abs(Lr).max()

@@ -159,6 +159,33 @@ def test_alpha(engine, nrhs):
     assert not np.any(a[n:])
 
 
+@pytest.mark.parametrize("n,nrhs,kind", [(1, 1, "rbf"), (128, 2, "matern52"), (333, 1, "rbf"), (1100, 8, "rbf"),
+                                         (2500, 3, "scale_linear_matern52"), (4096, 1, "rbf")])
+def test_potrs_alpha_matches_inverse_path_and_oracle(engine, n, nrhs, kind):
+    """alpha by the triangular solves on L (gpx_fit_factor_f64 / gpx_potrs_f64, no W) against alpha = W W^T (y - m) of
+    the inverse path (gpx_fit_f64) and the oracle; the factor-only state builds the same W on first use."""
+    d = 5
+    X, y = O.synthetic_problem(n, d, 40 + n)
+    Y = np.stack([y * (r + 1) - 0.3 * r for r in range(nrhs)], 1)
+    kp, op = pair(kind, d, noise=1e-3, const_mean=-0.2)
+    st = engine.fit(t(X), t(Y), kp)  # factor only
+    assert not st.W_ready
+    full = engine.fit(t(X), t(Y), kp, inverse=True)
+    a, af = st.alpha.cpu().numpy(), full.alpha.cpu().numpy()
+    assert torch.equal(torch.tril(st.L), torch.tril(full.L))
+    assert np.abs(a - af).max() <= 1e-10 * np.abs(af).max()
+    ar = O.fit(X, Y, op).alpha.reshape(n, nrhs)
+    assert np.abs(a[:n] - ar).max() <= 1e-8 * np.abs(ar).max()
+    assert not np.any(a[n:])
+    # the standalone solve on the same factor, new targets: same alpha as a refit with them
+    Y2 = Y[:, :1] * 0.5 + 0.1
+    a2 = engine.potrs(st, t(Y2)).cpu().numpy()
+    ar2 = O.fit(X, Y2, op).alpha.reshape(n, 1)
+    assert np.abs(a2[:n] - ar2).max() <= 1e-8 * np.abs(ar2).max()
+    engine.inverse(st)
+    assert torch.equal(torch.triu(st.W), torch.triu(full.W))
+
+
 # ---- posterior ----------------------------------------------------------------------------------------
 @pytest.mark.parametrize("kind", list(KINDS))
 @pytest.mark.parametrize("n,d,m,nrhs", [(1, 2, 1, 1), (150, 5, 777, 2), (513, 8, 3000, 8), (1024, 16, 256, 1)])
@@ -389,8 +416,9 @@ def test_config5_fp32_build_ucb_sweep(engine):
 
 
 # ---- batched fits (BASELINE configs[3] shape) ------------------------------------------------------------
+@pytest.mark.parametrize("inverse", [False, True])
 @pytest.mark.parametrize("n,B,nrhs", [(300, 3, 1), (1000, 4, 2), (129, 5, 1)])
-def test_fit_batched_matches_single_fits_and_oracle(engine, n, B, nrhs):
+def test_fit_batched_matches_single_fits_and_oracle(engine, n, B, nrhs, inverse):
     d = 6
     kp, op = pair("matern52", d, noise=2e-4)
     Xs, Ys = [], []
@@ -398,9 +426,12 @@ def test_fit_batched_matches_single_fits_and_oracle(engine, n, B, nrhs):
         X, y = O.synthetic_problem(n, d, 100 + b)
         Xs.append(X)
         Ys.append(np.stack([y * (r + 1) + r for r in range(nrhs)], axis=1))
-    sts = engine.fit_batched(t(np.stack(Xs)), t(np.stack(Ys)), kp)
+    sts = engine.fit_batched(t(np.stack(Xs)), t(np.stack(Ys)), kp, inverse=inverse)
     for b in range(B):
-        single = engine.fit(t(Xs[b]), t(Ys[b]), kp)
+        single = engine.fit(t(Xs[b]), t(Ys[b]), kp, inverse=inverse)
+        assert sts[b].W_ready == inverse
+        engine.inverse(sts[b])
+        engine.inverse(single)
         # same kernels, same inputs: identical factor, inverse and alpha
         assert torch.equal(torch.tril(sts[b].L[:n, :n]), torch.tril(single.L[:n, :n]))
         assert torch.equal(torch.triu(sts[b].W), torch.triu(single.W))  # W is defined on its upper triangle
@@ -428,6 +459,8 @@ def test_configs3_per_gpu_share_batched_n4096(engine):
     for b, (X, y) in enumerate(probs):
         single = engine.fit(t(X), t(y), kp)
         assert torch.equal(torch.tril(sts[b].L), torch.tril(single.L))
+        engine.inverse(sts[b])
+        engine.inverse(single)
         assert torch.equal(torch.triu(sts[b].W), torch.triu(single.W))
         assert torch.equal(sts[b].alpha, single.alpha)
         del single
@@ -482,6 +515,7 @@ def test_large_fit_inverse_and_factor_rows(engine, n, kind):
     Kr[np.arange(16), rows] += op.noise
     assert np.abs((Lt[ri] @ Lt.T).cpu().numpy() - Kr).max() <= 1e-11
     # (L^{-1} L)[rows] = I[rows] with L^{-1} = W^T
+    engine.inverse(st)
     prod = torch.triu(st.W[:n, :n]).T[ri] @ Lt
     eye = torch.zeros_like(prod)
     eye[torch.arange(16, device=DEV), ri] = 1.0

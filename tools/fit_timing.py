@@ -18,15 +18,18 @@ Xt, yt = torch.tensor(X, device=dev), torch.tensor(y, device=dev)
 st = eng.fit(Xt, yt, p)
 torch.cuda.synchronize()
 eng.timing_enable(["gram", "potrf", "trtri", "alpha"])
-ts = []
-for r in range(a.reps):
-    eng.timing_reset()
-    t0 = time.perf_counter()
-    st = eng.fit(Xt, yt, p, check=False, out=st)
-    torch.cuda.synchronize()
-    ts.append(time.perf_counter() - t0)
-    parts = {k: eng.timing_query(k)[0] for k in ["gram", "potrf", "trtri", "alpha"]}
-print(f"n={a.n} fit: {1e3*min(ts):.2f} ms (best of {a.reps}); " + ", ".join(f"{k} {v:.2f} ms" for k, v in parts.items()))
+for inverse in (False, True):
+    ts = []
+    for r in range(a.reps):
+        eng.timing_reset()
+        t0 = time.perf_counter()
+        st = eng.fit(Xt, yt, p, check=False, out=st, inverse=inverse)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+        parts = {k: eng.timing_query(k)[0] for k in ["gram", "potrf", "trtri", "alpha"]}
+    what = "fit + L^-T (gpx_fit_f64)" if inverse else "update (gpx_fit_factor_f64: alpha by potrs)"
+    print(f"n={a.n} {what}: {1e3*min(ts):.3f} ms (best of {a.reps}); " +
+          ", ".join(f"{k} {v:.3f} ms" for k, v in parts.items()))
 flops = a.n ** 3 / 3
 print(f"  potrf {flops / (parts['potrf'] * 1e-3) / 1e12:.1f} TF/s, trtri {flops / (parts['trtri'] * 1e-3) / 1e12:.1f} TF/s (n^3/3 each)")
 # residual on sampled rows: (L L^T)[rows] vs K[rows]
