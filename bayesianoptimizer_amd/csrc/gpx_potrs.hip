@@ -77,6 +77,31 @@ __device__ __forceinline__ void publish_block(gu64* g, unsigned epoch, const dou
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Lane exchanges inside groups of 8 lanes by DPP (VALU, no LDS round trip like __shfl_xor's ds_bpermute):
+// xor 1 / xor 2 by quad_perm, xor 4 by row_shl:4 into banks 0/2 and row_shr:4 into banks 1/3.
+template <int CTRL, int BANKS>
+__device__ __forceinline__ unsigned dpp_u32(unsigned old, unsigned x) {
+  return (unsigned)__builtin_amdgcn_update_dpp((int)old, (int)x, CTRL, 0xf, BANKS, false);
+}
+template <int X>
+__device__ __forceinline__ double xor_lane(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+  unsigned rlo, rhi;
+  if constexpr (X == 1) {
+    rlo = dpp_u32<0xB1, 0xf>(0u, lo);
+    rhi = dpp_u32<0xB1, 0xf>(0u, hi);
+  } else if constexpr (X == 2) {
+    rlo = dpp_u32<0x4E, 0xf>(0u, lo);
+    rhi = dpp_u32<0x4E, 0xf>(0u, hi);
+  } else {
+    static_assert(X == 4, "xor 1, 2 or 4");
+    rlo = dpp_u32<0x114, 0xA>(dpp_u32<0x104, 0x5>(0u, lo), lo);
+    rhi = dpp_u32<0x114, 0xA>(dpp_u32<0x104, 0x5>(0u, hi), hi);
+  }
+  return __longlong_as_double(((unsigned long long)rhi << 32) | rlo);
+}
+
 // 64x64 tile of a row-major global matrix into LDS (row length LDT)
 __device__ __forceinline__ void tile_to_lds(const double* __restrict__ G, int64_t ld, double* S) {
   for (int e = threadIdx.x; e < NB * NB / 2; e += WG) {
@@ -348,12 +373,12 @@ __device__ void potrs_items_1(int n, int npad, const double* __restrict__ L, int
     if (fwd) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        acc[k][0] += __shfl_xor(acc[k][0], 1);
-        acc[k][0] += __shfl_xor(acc[k][0], 2);
-        acc[k][0] += __shfl_xor(acc[k][0], 4);
+        acc[k][0] += xor_lane<1>(acc[k][0]);
+        acc[k][0] += xor_lane<2>(acc[k][0]);
+        acc[k][0] += xor_lane<4>(acc[k][0]);
       }
     } else {
-      acc[0][0] += __shfl_xor(acc[0][0], 1);
+      acc[0][0] += xor_lane<1>(acc[0][0]);
     }
     __syncthreads();  // s.vs (right-hand side) complete
     if (fwd) {
@@ -390,9 +415,9 @@ __device__ void potrs_items_1(int n, int npad, const double* __restrict__ L, int
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        z[k] += __shfl_xor(z[k], 1);
-        z[k] += __shfl_xor(z[k], 2);
-        z[k] += __shfl_xor(z[k], 4);
+        z[k] += xor_lane<1>(z[k]);
+        z[k] += xor_lane<2>(z[k]);
+        z[k] += xor_lane<4>(z[k]);
         if (aborted) z[k] = __builtin_nan("");
       }
       GPX_POTRS_STAMP(3);
@@ -422,7 +447,7 @@ __device__ void potrs_items_1(int n, int npad, const double* __restrict__ L, int
         }
       }
       double a = a0 + a1;
-      a += __shfl_xor(a, 1);
+      a += xor_lane<1>(a);
       if (aborted) a = __builtin_nan("");
       GPX_POTRS_STAMP(3);
       const unsigned long long u = __double_as_longlong(a);
