@@ -178,6 +178,17 @@ struct MfmaTile {
     }
   }
 
+  // acc = -C (C: the TM x TN tile at Cg, row-major, leading dimension ldc): every load issued at once, so a following
+  // run_acc(...) leaves acc = A B - C with no load round trip after the k loop (the caller stores -acc).
+  __device__ __forceinline__ void load_neg_c(const double* __restrict__ Cg, int64_t ldc) {
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = -Cg[(int64_t)row_of(i, r) * ldc + col_of(j)];
+  }
+
   // Full k loop. smem must hold LDS_DOUBLES doubles.  A/B point at the tile origin (m0 / n0 applied).
   // One loop body with swapped current/next LDS pointers: the two-branch (even/odd buffer) form made hipcc
   // rename the accumulators between branches and shuttle them through AGPR moves after dependent MFMAs
@@ -185,6 +196,12 @@ struct MfmaTile {
   __device__ __forceinline__ void run(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
                                       int64_t ldb, int kbeg, int kend, double* smem) {
     zero();
+    run_acc(A, lda, B, ldb, kbeg, kend, smem);
+  }
+
+  // The same k loop accumulating onto the current acc.
+  __device__ __forceinline__ void run_acc(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
+                                          int64_t ldb, int kbeg, int kend, double* smem) {
     if (kend <= kbeg) return;
     double* cur = smem;
     double* nxt = smem + BK * (PA + PB);

@@ -33,8 +33,35 @@
 #ifndef GPX_PANEL_STAMP
 #define GPX_PANEL_STAMP(i)
 #endif
+#ifndef GPX_PERSIST_STAMP
+#define GPX_PERSIST_STAMP(kind, c, i, s)
+#endif
 
 namespace gpx {
+
+// Write-through (sc1) stores through a raw buffer resource: one SGPR descriptor + a 32-bit lane offset per store (the
+// 64-bit-address atomic-store form of the same store pushed the persistent trailing role into scratch spills).
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kAuxSC1 = 16;  // cache-policy operand of the buffer intrinsics: sc1 (write-through, agent coherent)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+}
+#ifndef GPX_PROBE_PLAIN_STORES  // timing experiments only (tools/potrf_probe.hip); never defined in the library
+constexpr int kStoreAux = kAuxSC1;
+#else
+constexpr int kStoreAux = 0;
+#endif
+__device__ __forceinline__ void store_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, double v) {
+  const unsigned long long b = __double_as_longlong(v);
+  const u32x2 x = {(unsigned)b, (unsigned)(b >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(x, r, byte_off, 0, kStoreAux);
+}
+__device__ __forceinline__ void store_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, double v0, double v1) {
+  const unsigned long long b0 = __double_as_longlong(v0), b1 = __double_as_longlong(v1);
+  const u32x4 x = {(unsigned)b0, (unsigned)(b0 >> 32), (unsigned)b1, (unsigned)(b1 >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b128(x, r, byte_off, 0, kStoreAux);
+}
 
 using Tile64 = MfmaTile<NB, NB, 16, false, false>;        // panel-side update (one 64x64 tile)
 using Tile128 = MfmaTile<2 * NB, 2 * NB, 16, false, false>;  // trailing update
@@ -48,21 +75,23 @@ static_assert(NB * LD64 + DBUF >= Tile64::LDS_DOUBLES && DBUF >= 2 * 16 * LDD, "
 constexpr int PANEL_LDS = 2 * NB * LD64 + DBUF;
 constexpr int STEP_LDS = PANEL_LDS > Tile128::LDS_DOUBLES ? PANEL_LDS : Tile128::LDS_DOUBLES;
 
-// C (64x64 at Cg, global) - acc  -> LDS tile S (row length LD64)
-__device__ __forceinline__ void tile_sub_to_lds(const Tile64& tl, const double* __restrict__ Cg, int64_t ldc, double* S) {
-  double cv[Tile64::WM][Tile64::WN][4];
+// C - L_a L_b^T for a 64x64 tile into the LDS tile S (row length LD64): acc seeded with -C (its loads issued with the
+// first k-tile's, no load round trip after the product), acc += L_a L_b^T over K, S = -acc.
+__device__ __forceinline__ void update_to_lds(Tile64& tl, const double* __restrict__ Cg, int64_t ldc,
+                                              const double* __restrict__ La, const double* __restrict__ Lb, int64_t ldl,
+                                              int K, double* smem, double* S) {
+  tl.load_neg_c(Cg, ldc);
+  if (K == NB)
+    tl.run_acc(La, ldl, Lb, ldl, 0, NB, smem);  // the eager case, on the critical path: compile-time trip count
+  else
+    tl.run_acc(La, ldl, Lb, ldl, 0, K, smem);
+  // run_acc() ends with a barrier after its last LDS read, so S may alias the staging
 #pragma unroll
   for (int i = 0; i < Tile64::WM; ++i)
 #pragma unroll
     for (int j = 0; j < Tile64::WN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) cv[i][j][r] = Cg[(int64_t)Tile64::row_of(i, r) * ldc + Tile64::col_of(j)];
-#pragma unroll
-  for (int i = 0; i < Tile64::WM; ++i)
-#pragma unroll
-    for (int j = 0; j < Tile64::WN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) S[Tile64::row_of(i, r) * LD64 + Tile64::col_of(j)] = cv[i][j][r] - tl.acc[i][j][r];
+      for (int r = 0; r < 4; ++r) S[Tile64::row_of(i, r) * LD64 + Tile64::col_of(j)] = -tl.acc[i][j][r];
 }
 
 __device__ __forceinline__ void load_tile_lds(const double* __restrict__ G, int64_t ld, double* S) {
@@ -76,7 +105,9 @@ __device__ __forceinline__ void load_tile_lds(const double* __restrict__ G, int6
   }
 }
 
-// Panel workgroup p of block column c (see the file comment).
+// Panel workgroup p of block column c (see the file comment).  SC1: the L_ic tile is stored write-through (agent-scope
+// atomic 8-byte stores) for the in-launch hand-off of the persistent schedule.
+template <bool SC1 = false>
 __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, int c, int p, int nblk, int c0,
                                            double* __restrict__ Dinv, int32_t* __restrict__ info, double* lds) {
   double* sA = lds;             // A_cc -> L_cc
@@ -97,21 +128,11 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
     const int kk = (c - c0) * NB;
     const double* Lc = A + (int64_t)c * NB * lda + (int64_t)c0 * NB;
     Tile64 tl;
-    // K = 64 (the eager case, on the critical path of every step) with a compile-time trip count
-    if (kk == NB)
-      tl.run(Lc, lda, Lc, lda, 0, NB, smem);
-    else
-      tl.run(Lc, lda, Lc, lda, 0, kk, smem);
-    tile_sub_to_lds(tl, Acc, lda, sA);
+    update_to_lds(tl, Acc, lda, Lc, Lc, lda, kk, smem, sA);
     if (panel) {
       __syncthreads();  // smem reuse
       const double* Li = A + (int64_t)bi * NB * lda + (int64_t)c0 * NB;
-      if (kk == NB)
-        tl.run(Li, lda, Lc, lda, 0, NB, smem);
-      else
-        tl.run(Li, lda, Lc, lda, 0, kk, smem);
-      // run() ends with a barrier after its last LDS read, so the epilogue may overwrite the staging (sP)
-      tile_sub_to_lds(tl, Aic, lda, sP);
+      update_to_lds(tl, Aic, lda, Li, Lc, lda, kk, smem, sP);
     }
   } else {
     load_tile_lds(Acc, lda, sA);
@@ -187,7 +208,11 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int e = (t + q * WG) * 2, r = e >> 6, cc = e & 63;
-    *reinterpret_cast<double2*>(Aic + (int64_t)r * lda + cc) = make_double2(sP[r * LD64 + cc], sP[r * LD64 + cc + 1]);
+    if (SC1) {
+      store_sc1(rsrc_of(Aic), (int)(((int64_t)r * lda + cc) * 8), sP[r * LD64 + cc], sP[r * LD64 + cc + 1]);
+    } else {
+      *reinterpret_cast<double2*>(Aic + (int64_t)r * lda + cc) = make_double2(sP[r * LD64 + cc], sP[r * LD64 + cc + 1]);
+    }
   }
 }
 
@@ -208,7 +233,8 @@ __device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t ld
   double* C = A + (int64_t)r0 * NB * lda + (int64_t)q0 * NB;
   Tile128 tl;
   tl.run(Li, lda, Lj, lda, 0, lazy * NB, lds);
-  // C - acc, stored for the 64-blocks (rb, cb) with cb >= c+1 and rb >= cb; loads of a row group first
+  // C - acc, stored for the 64-blocks (rb, cb) with cb >= c+1 and rb >= cb; loads of a row group first (seeding acc with
+  // -C before the product, as the 64x64 panel updates do, pushes this 128x128 tile into 30 VGPR spills)
 #pragma unroll
   for (int i = 0; i < Tile128::WM; ++i) {
     double cv[Tile128::WN][4];
@@ -237,16 +263,215 @@ __device__ __forceinline__ void lookahead_role(double* __restrict__ A, int64_t l
   const double* Lj = A + (int64_t)j * NB * lda + (int64_t)a * NB;
   double* C = A + (int64_t)i * NB * lda + (int64_t)j * NB;
   Tile64 tl;
-  tl.run(Li, lda, Lj, lda, 0, (c - a) * NB, lds);
+  tl.load_neg_c(C, lda);
+  tl.run_acc(Li, lda, Lj, lda, 0, (c - a) * NB, lds);
 #pragma unroll
   for (int ii = 0; ii < Tile64::WM; ++ii)
 #pragma unroll
     for (int jj = 0; jj < Tile64::WN; ++jj)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        double* Cp = C + (int64_t)Tile64::row_of(ii, r) * lda + Tile64::col_of(jj);
-        *Cp = *Cp - tl.acc[ii][jj][r];
+      for (int r = 0; r < 4; ++r) C[(int64_t)Tile64::row_of(ii, r) * lda + Tile64::col_of(jj)] = -tl.acc[ii][jj][r];
+}
+
+// ---- persistent dataflow schedule (one launch for the whole factorisation) ------------------------------------
+// VERDICT r1 "next 3": the 64 dependent launches of the eager schedule each last as long as their slowest trailing tile
+// (31-46 us in steps 1-22 at n = 4096 against a ~15 us panel chain), plus a launch boundary.  Here ONE launch holds
+//  * nblk panel workgroups: workgroup i runs the panel tasks P(c, i), c = 0 .. i, of its row block in order (exactly
+//    panel_role's work with c0 = c-1: the column c-1 update of tiles (c, c) and (i, c), the in-LDS factorisation, L_ic
+//    stored) and publishes pdone[c][i];
+//  * NT trailing workgroups: the tasks U(c, I, J) = "apply column c to the 128x128 tile (I, J)" for every tile whose
+//    block columns reach c+2, in the order (c, J, I), dealt round robin (task k -> workgroup k mod NT), each bumping
+//    the tile's version counter.
+// Dependencies: P(c, i) waits for pdone[c-1][c] (L_{c,c-1}) and for the versions of the tiles holding (c, c) and
+// (i, c) to reach c-1 (updates 0 .. c-2 applied; its own previous task produced L_{i,c-1}); U(c, I, J) waits for
+// pdone[c][rows 2I, 2I+1, 2J, 2J+1] and for the tile's version to equal c (updates to a tile are applied in column
+// order).  Every task waits only on tasks that precede it in its pool's order or on the other pool's earlier tasks,
+// and the grid is sized to be co-resident (<= 2 workgroups per CU, 75 KB LDS each), so the schedule cannot deadlock;
+// every spin is bounded and gives up (info = -1) rather than hang.
+// Hand-offs follow cdna_hip_programming.md §6 Guideline 16 (R1): payload stores write-through (agent-scope atomic
+// stores), every storing wave drains (s_waitcnt vmcnt(0)), a barrier, then ONE lane stores the flag / version; the
+// consumer polls relaxed from one wave, then ONE agent-scope acquire, vmcnt(0), barrier, plain loads.
+// The arithmetic, and its order, is the eager schedule's: L is bit-identical to the multi-launch path.
+struct SyncWords {
+  int* base;  // nblk * nblk pdone flags, then the 128-tile versions, then the timeout word
+  int nblk;
+  __device__ int* pdone(int c, int i) const { return base + c * nblk + i; }
+  __device__ int* ver(int I, int J) const { return base + nblk * nblk + I * (I + 1) / 2 + J; }
+  __device__ int* timeout() const { const int M = nblk / 2; return base + nblk * nblk + M * (M + 1) / 2; }
+};
+
+__host__ __device__ inline int sync_word_count(int nblk) {
+  const int M = nblk / 2;
+  return nblk * nblk + M * (M + 1) / 2 + 1;
+}
+
+constexpr unsigned kPotrfSpinLimit = 1u << 23;
+
+// One wave polls: lane k waits for *mine >= want (lanes with mine == nullptr are satisfied); the other waves of the
+// workgroup meet it at the barrier that follows the acquire.  Returns false when the timeout word is (or gets) set.
+__device__ __forceinline__ bool poll_ge(const SyncWords& sw, int* mine, int want) {
+  const int lane = threadIdx.x & 63;
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+    if (mine) ok = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
+    if (__all(ok)) return true;
+    if ((spins & 255) == 255) {
+      if (__hip_atomic_load(sw.timeout(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
+      if (spins >= kPotrfSpinLimit) {
+        if (lane == 0) __hip_atomic_store(sw.timeout(), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
       }
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// Wave 0 polls (its lanes' words), then the acquire that makes the other workgroups' write-through stores visible to
+// this CU's plain loads, then a barrier for the other waves.  Returns false (uniformly) on timeout.
+__device__ __forceinline__ bool wait_and_acquire(const SyncWords& sw, int* mine, int want) {
+  __shared__ int s_ok;
+  if (threadIdx.x < 64) {
+    const bool ok = poll_ge(sw, mine, want);
+#ifndef GPX_PROBE_NO_ACQUIRE  // timing experiments only (tools/potrf_probe.hip); never defined in the library
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) s_ok = ok ? 1 : 0;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+// Every storing wave drains its write-through stores, a barrier, then one lane publishes `value` into *word.
+__device__ __forceinline__ void publish(int* word, int value) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(word, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// U(c, I, J): tile (I, J) of the 128-grid -= L_{rows, c} L_{cols, c}^T, stored (write-through) for the 64-blocks
+// (rb, cb) with cb >= c+2 and rb >= cb.
+__device__ __forceinline__ void persist_update(double* __restrict__ A, int64_t lda, int c, int I, int J, double* lds) {
+  const int r0 = 2 * I, q0 = 2 * J;
+  const double* Li = A + (int64_t)r0 * NB * lda + (int64_t)c * NB;
+  const double* Lj = A + (int64_t)q0 * NB * lda + (int64_t)c * NB;
+  double* C = A + (int64_t)r0 * NB * lda + (int64_t)q0 * NB;
+  const __amdgpu_buffer_rsrc_t rc = rsrc_of(C);
+  Tile128 tl;
+  // acc = -C, loads issued together with the first k-tile's, then acc += L_i L_j^T: C - L_i L_j^T = -acc, stored with
+  // no load round trip after the k loop (an epilogue that loaded C after the product spent 30-45 us per task waiting
+  // on the Infinity Cache)
+  tl.load_neg_c(C, lda);
+  tl.run_acc(Li, lda, Lj, lda, 0, NB, lds);
+#pragma unroll
+  for (int i = 0; i < Tile128::WM; ++i)
+#pragma unroll
+    for (int j = 0; j < Tile128::WN; ++j) {
+      const int col = Tile128::col_of(j), cb = q0 + (col >> 6);
+      if (cb < c + 2) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = Tile128::row_of(i, r), rb = r0 + (row >> 6);
+        if (rb >= cb) store_sc1(rc, (int)(((int64_t)row * lda + col) * 8), -tl.acc[i][j][r]);
+      }
+    }
+}
+
+// First 128-tile column that U(c, ., .) touches, and its task count.
+__device__ __forceinline__ int ucol0(int c) { return (c + 2) / 2; }
+__device__ __forceinline__ int utasks(int c, int M) {
+  const int m = M - ucol0(c);
+  return m > 0 ? m * (m + 1) / 2 : 0;
+}
+
+__device__ __forceinline__ void persist_panel_loop(double* __restrict__ A, int64_t lda, int nblk, int i,
+                                                double* __restrict__ Dinv, int32_t* __restrict__ info, SyncWords sw,
+                                                double* lds) {
+  // panel workgroup of row block i: P(0, i), P(1, i), ..., P(i, i)
+  __builtin_amdgcn_s_setprio(3);
+  for (int c = 0; c <= i; ++c) {
+    // lane 0: L_{c,c-1} published (its own L_{i,c-1} came from its previous task); lanes 1 / 2: updates 0 .. c-2
+    // applied to the tiles holding (c, c) and (i, c)
+    const int lane = threadIdx.x & 63;
+    int* mine = nullptr;
+    int want = 0;
+    if (c > 0) {
+      if (lane == 0) {
+        mine = sw.pdone(c - 1, c);
+        want = 1;
+      } else if (lane == 1) {
+        mine = sw.ver(c / 2, c / 2);
+        want = c - 1;
+      } else if (lane == 2) {
+        mine = sw.ver(i / 2, c / 2);
+        want = c - 1;
+      }
+    }
+    GPX_PERSIST_STAMP(0, c, i, 0);
+    const bool ok = wait_and_acquire(sw, mine, want);
+    GPX_PERSIST_STAMP(0, c, i, 1);
+    if (!ok && threadIdx.x == 0) atomicCAS(info, 0, -1);
+    if (ok && __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+      panel_role<true>(A, lda, c, i - c, nblk, c > 0 ? c - 1 : 0, Dinv, info, lds);
+    GPX_PERSIST_STAMP(0, c, i, 2);
+    publish(sw.pdone(c, i), 1);
+    GPX_PERSIST_STAMP(0, c, i, 3);
+    __syncthreads();  // LDS reuse by the next task
+  }
+}
+
+__device__ __forceinline__ void persist_trailing_loop(double* __restrict__ A, int64_t lda, int nblk, int tw, int NT,
+                                                   int32_t* __restrict__ info, SyncWords sw, double* lds) {
+  // trailing workgroup: tasks k = tw, tw + NT, ... of the (c, J, I)-ordered list
+  const int M = nblk / 2;
+  int c = 0, base = 0;  // tasks of columns < c
+  for (int k = tw;; k += NT) {
+    while (c < nblk && k >= base + utasks(c, M)) base += utasks(c++, M);
+    if (c >= nblk) break;
+    // decode the task inside column c: J ascending from ucol0(c), then I from J
+    int r = k - base, J = ucol0(c);
+    while (r >= M - J) r -= M - J++;
+    const int I = J + r;
+    // lanes 0-3: L_{r, c} published for the tile's rows 2I, 2I+1 and columns 2J, 2J+1; lane 4: the tile's version = c
+    const int lane = threadIdx.x & 63;
+    int* mine = nullptr;
+    int want = 1;
+    if (lane < 4) mine = sw.pdone(c, lane < 2 ? 2 * I + lane : 2 * J + lane - 2);
+    else if (lane == 4) {
+      mine = sw.ver(I, J);
+      want = c;
+    }
+    GPX_PERSIST_STAMP(1, c, I * 64 + J, 0);
+    const bool ok = wait_and_acquire(sw, mine, want);
+    GPX_PERSIST_STAMP(1, c, I * 64 + J, 1);
+    if (!ok && threadIdx.x == 0) atomicCAS(info, 0, -1);
+    if (ok && __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+      persist_update(A, lda, c, I, J, lds);
+    GPX_PERSIST_STAMP(1, c, I * 64 + J, 2);
+    publish(sw.ver(I, J), c + 1);
+    GPX_PERSIST_STAMP(1, c, I * 64 + J, 3);
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
+potrf_persist_kernel(double* __restrict__ A, int64_t lda, int nblk, int npanel_wg, double* __restrict__ Dinv,
+                     int32_t* __restrict__ info, int* __restrict__ sync, int64_t sa, int64_t sd, int64_t ss) {
+  A += blockIdx.y * sa;  // problem of a batched fit
+  Dinv += blockIdx.y * sd;
+  info += blockIdx.y;
+  const SyncWords sw{sync + blockIdx.y * ss, nblk};
+  __shared__ __attribute__((aligned(16))) double lds[STEP_LDS];
+  const int b = blockIdx.x;
+  if (b < npanel_wg)
+    persist_panel_loop(A, lda, nblk, b, Dinv, info, sw, lds);
+  else
+    persist_trailing_loop(A, lda, nblk, b - npanel_wg, gridDim.x - npanel_wg, info, sw, lds);
+}
+
+__global__ void potrf_sync_clear_kernel(int* __restrict__ sync, int words, int64_t ss) {
+  int* p = sync + blockIdx.y * ss;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < words; e += gridDim.x * blockDim.x) p[e] = 0;
 }
 
 // Work split of launch c.  mode 0: the panels apply the pending columns c0 .. c-1 (c0 = the last flush), the flush
@@ -383,11 +608,40 @@ static void launch_dinv(Context* ctx, int nblk, double* A, int64_t lda, double* 
                                                                       bt.w);
 }
 
+// Persistent schedule: opt-in (GPX_POTRF_PERSIST=1) for 4 <= nblk <= 128 when the panel workgroups plus >= 64
+// trailing workgroups per problem fit in two workgroups per CU.  Measured slower than the multi-launch schedule
+// (n = 4096: 2.52 vs 1.74 ms): in the combined kernel the 128x128 trailing tasks spill (~120 VGPRs) and run
+// ~40 us instead of ~20, and the panel tasks ~22 us instead of ~15, which outweighs the removed launch boundaries.
+static int persist_grid(int nblk, int batch) {
+  static const int env = env_int("GPX_POTRF_PERSIST");
+  if (env != 1 || nblk > 128 || nblk < 4) return 0;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
+    cus = prop.multiProcessorCount;
+  }
+  const int per = 2 * cus / batch;  // co-resident workgroups per problem
+  return per - nblk >= 64 ? per : 0;
+}
+
 hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
                         double* W, int64_t ldw) {
   LaunchTimer tm(ctx, GPX_TIMER_POTRF);
   const int nblk = npad / NB;
-  launch_steps(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk);
+  const int grid = persist_grid(nblk, bt.count);
+  if (grid) {
+    // the sync words live in the first half of Dinv (written by potrf_dinv only after the factorisation)
+    int* sync = reinterpret_cast<int*>(Dinv);
+    const int words = sync_word_count(nblk);
+    const int64_t ss = 2 * bt.dinv;  // ints per problem
+    potrf_sync_clear_kernel<<<dim3((words + 1023) / 1024, bt.count), 1024 / 4, 0, ctx->stream>>>(sync, words, ss);
+    potrf_persist_kernel<<<dim3(grid, bt.count), WG, 0, ctx->stream>>>(A, lda, nblk, nblk, Dinv, info, sync, bt.k,
+                                                                       bt.dinv, ss);
+  } else {
+    launch_steps(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk);
+  }
   launch_dinv(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, W, ldw);
   return hipGetLastError();
 }
