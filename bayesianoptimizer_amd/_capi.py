@@ -94,6 +94,9 @@ _PROTOS = {
     "gpx_potrf_f64": (c_int32, [_h, c_int64, _p, c_int64, _p, _p]),
     "gpx_trtri_workspace_size": (c_int32, [c_int64, POINTER(c_size_t)]),
     "gpx_trtri_f64": (c_int32, [_h, c_int64, _p, c_int64, _p, _p, c_int64, _p, c_size_t]),
+    "gpx_trtri_batched_workspace_size": (c_int32, [c_int64, c_int64, POINTER(c_size_t)]),
+    "gpx_trtri_batched_f64": (c_int32, [_h, c_int64, c_int64, _p, c_int64, c_int64, _p, c_int64, _p, c_int64, c_int64,
+                                        _p, c_size_t]),
     "gpx_alpha_workspace_size": (c_int32, [c_int64, c_int64, POINTER(c_size_t)]),
     "gpx_alpha_f64": (c_int32, [_h, c_int64, _p, c_int64, _p, c_int64, c_int64, c_double, _p, _p, c_size_t]),
     "gpx_fit_workspace_size": (c_int32, [c_int64, c_int64, POINTER(c_size_t)]),

@@ -237,6 +237,44 @@ gpx_status gpx_trtri_f64(gpx_handle h, int64_t n, const double* L, int64_t ldl, 
   return trtri_impl(h, n, L, ldl, Dinv, W, ldw, ws, ws_bytes, false);
 }
 
+gpx_status gpx_trtri_batched_workspace_size(int64_t n, int64_t batch, size_t* bytes) {
+  if (!bytes || n < 1 || batch < 1 || batch > 65535) return GPX_INVALID_ARG;
+  *bytes = ((trtri_ws(padded(n)) + 255) & ~(size_t)255) * (size_t)batch + 256;
+  return GPX_OK;
+}
+
+gpx_status gpx_trtri_batched_f64(gpx_handle h, int64_t batch, int64_t n, const double* L, int64_t ldl, int64_t stride_l,
+                                 const double* Dinv, int64_t stride_dinv, double* W, int64_t ldw, int64_t stride_w,
+                                 void* ws, size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_TRY(check_n(c, n));
+  if (batch < 1 || batch > 65535) return fail(c, GPX_INVALID_ARG, "batch must be in [1, 65535]");
+  GPX_NONNULL(c, L);
+  GPX_NONNULL(c, Dinv);
+  GPX_NONNULL(c, W);
+  GPX_NONNULL(c, ws);
+  const int64_t npad = padded(n);
+  GPX_TRY(check_ld(c, ldl, npad, "L", true));
+  GPX_TRY(check_ld(c, ldw, npad, "W", true));
+  if (batch > 1) {
+    if (stride_l < npad * ldl || stride_w < npad * ldw || stride_dinv < 2 * (npad / gpx::NB) * gpx::NB * gpx::NB)
+      return fail(c, GPX_INVALID_ARG, "batch strides smaller than one problem");
+    if ((stride_l | stride_w | stride_dinv) & 1) return fail(c, GPX_INVALID_ARG, "L/W/Dinv strides must be even");
+  }
+  size_t need = 0;
+  GPX_TRY(gpx_trtri_batched_workspace_size(n, batch, &need));
+  if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "batched trtri workspace too small");
+  GPX_USE_DEVICE(c);
+  gpx::Batch bt;
+  bt.count = (int)batch;
+  bt.k = stride_l;
+  bt.dinv = stride_dinv;
+  bt.w = stride_w;
+  bt.ws = (int64_t)(((trtri_ws(npad) + 255) & ~(size_t)255) / sizeof(double));
+  return hip_check(c, gpx::launch_trtri(c, (int)npad, L, ldl, Dinv, W, ldw, align256(ws), bt, false), "trtri");
+}
+
 gpx_status gpx_alpha_workspace_size(int64_t n, int64_t nrhs, size_t* bytes) {
   if (!bytes || n < 1 || nrhs < 1 || nrhs > GPX_MAX_RHS) return GPX_INVALID_ARG;
   *bytes = alpha_ws(padded(n), nrhs);

@@ -268,6 +268,34 @@ class GPEngine:
         state.W_ready = True
         return state
 
+    def inverse_batched(self, states: Sequence[GPState]) -> Sequence[GPState]:
+        """W for every state of one ``fit_batched`` call in the same launches (gpx_trtri_batched_f64); states that
+        already have W are left alone, states of different calls fall back to ``inverse`` one by one."""
+        todo = [st for st in states if not st.W_ready]
+        if not todo:
+            return states
+        b0 = todo[0]._batch
+        if b0 is None or len(todo) != len(states) or any(st._batch is not b0 for st in todo):
+            for st in todo:
+                self.inverse(st)
+            return states
+        Lb, Wb, Db, _, _ = b0
+        B, npad = Lb.shape[0], Lb.shape[1]
+        if B != len(states):
+            for st in todo:
+                self.inverse(st)
+            return states
+        n = states[0].n
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_trtri_batched_workspace_size(n, B, ctypes.byref(nbytes)))
+        ws = self.workspace("trtri_batched", nbytes.value)
+        self._bind_stream()
+        self._check(self.lib.gpx_trtri_batched_f64(self.handle, B, n, _ptr(Lb), npad, Lb.stride(0), _ptr(Db),
+                                                   Db.stride(0), _ptr(Wb), npad, Wb.stride(0), _ptr(ws), ws.numel()))
+        for st in states:
+            st.W_ready = True
+        return states
+
     def potrs(self, state: GPState, Y) -> torch.Tensor:
         """alpha = K^{-1}(Y - const_mean) from the state's factor alone (gpx_potrs_f64): new targets on the same X."""
         Y = self._as_f64(Y, "Y")

@@ -1,8 +1,9 @@
 """Benchmark of the GP-posterior hot path (BASELINE.json metric), one process per GPU.
 
-A step = one posterior update (Gram + blocked Cholesky + L^{-T} + alpha, n=4096, d=8, RBF, fp64) followed by
-a 2^20-candidate analytic logEI sweep with argmax (BASELINE.json configs[1]), then the cross-rank (value,
-index) exchange.  Every rank owns an independent problem (different seed: weak scaling); the
+A step = one posterior update (Gram + blocked Cholesky + alpha by triangular solves, n=4096, d=8, RBF, fp64;
+SURVEY §8d's unit) followed by a 2^20-candidate analytic logEI sweep with argmax (BASELINE.json configs[1]) —
+which first builds the explicit inverse L^{-T} its triangular product needs — then the cross-rank (value, index)
+exchange.  Every rank owns an independent problem (different seed: weak scaling); the
 only collective is an all-gather of one 16-byte record per rank over RCCL.
 
 Prints ONE JSON line on rank 0.  value = candidates scored per second over the whole job
@@ -180,9 +181,15 @@ def other_configs(eng, dev, seed):
     if st.pivot_failure() >= 0:
         raise RuntimeError("configs[2] Cholesky failed")
     t = float(np.median(ts))
-    out["configs[2]"] = {"workload": "n=16384 d=8 Matern-5/2 fp64 posterior update (Gram + Cholesky + L^-T + alpha)",
-                         "fit_ms": 1e3 * t, "updates_per_s": 1.0 / t,
-                         "cholesky_plus_inverse_tflops": 2 * 16384.0 ** 3 / 3 / t / 1e12}
+    torch.cuda.synchronize()
+    a = time.perf_counter()
+    eng.inverse(st)  # what the first sweep after this update would add
+    torch.cuda.synchronize()
+    ti = time.perf_counter() - a
+    out["configs[2]"] = {"workload": "n=16384 d=8 Matern-5/2 fp64 posterior update (Gram + Cholesky + alpha by "
+                                     "triangular solves)", "fit_ms": 1e3 * t, "updates_per_s": 1.0 / t,
+                         "update_tflops_n3_over_3": 16384.0 ** 3 / 3 / t / 1e12,
+                         "inverse_ms_for_a_following_sweep": 1e3 * ti}
     del st, X, y
     torch.cuda.empty_cache()
     X_np, y_np = synthetic.problem(4096, 16, seed + 11)
@@ -273,6 +280,7 @@ def other_configs(eng, dev, seed):
 
     def share_step():
         ss = eng.fit_batched(Xb, yb, p, check=False, out=sts)
+        eng.inverse_batched(ss)
         for q in range(P4):
             v, i = eng.acquire(ss[q], Xs4[q], "logei", best_f=bf4[q], index_offset=q << 20)
             lv[q:q + 1].copy_(v)
@@ -298,7 +306,8 @@ def other_configs(eng, dev, seed):
     f, t = float(np.median(tf)), float(np.median(ts))
     out["configs[3] per-GPU share"] = {
         "workload": "4 independent n=4096 d=8 RBF fp64 problems per GPU (32 restarts / 8 GPUs), batched posterior "
-                    "update + a 1048576-candidate logEI sweep each + argmax combine",
+                    "update (batched_fit_ms), then batched L^-T + a 1048576-candidate logEI sweep each + argmax "
+                    "combine (ms_per_step)",
         "problems": P4, "batched_fit_ms": 1e3 * f, "updates_per_s": P4 / f, "ms_per_step": 1e3 * t,
         "acq_cands_per_s": P4 * (1 << 20) / t, "best_index": int(bi.item())}
     del sts, Xb, yb, Xs4
@@ -364,6 +373,8 @@ def main():
 
     def step():
         sts = fit_all()
+        if P > 1:
+            eng.inverse_batched(sts)  # W = L^-T of every problem for its sweep, in the same launches
         for q, (Xq, yq, Xsq, bfq, unit) in enumerate(probs):
             bv, bi = eng.acquire(sts[q], Xsq, args.acq, best_f=bfq, index_offset=unit * args.m)
             loc_v[q:q + 1].copy_(bv)
@@ -397,6 +408,13 @@ def main():
         fit_all()
     barrier(dist)
     fit_elapsed = time.perf_counter() - t2
+    # per-kernel split of the update (hipEvents around each family, a separate loop so the timed one is event-free)
+    eng.timing_reset()
+    eng.timing_enable(["gram", "potrf", "alpha"])
+    for _ in range(fit_reps):
+        fit_all()
+    part = {k: eng.timing_query(k) for k in ("gram", "potrf", "alpha")}
+    eng.timing_disable()
 
     times = torch.tensor([elapsed, fit_elapsed], dtype=torch.float64, device=dev)
     if dist is not None:
@@ -416,6 +434,9 @@ def main():
         kstar_bytes = 8.0 * (npad * kc + (n + kc) * args.d)
         kstar_avg = kstar_ms / max(kstar_launches, 1)
         kstar_gbs = kstar_bytes / (kstar_avg * 1e-3) / 1e9
+        gram_bytes = P * 8.0 * (npad * (npad + 1) / 2 + n * args.d)
+        gram_avg = part["gram"][0] / max(part["gram"][1], 1)
+        gram_gbs = gram_bytes / (gram_avg * 1e-3) / 1e9
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(X_np, y_np, Xs_np, args.kernel, args.acq, ls, args.cpu_sample)
@@ -446,9 +467,11 @@ def main():
             },
             "updates_per_s": world * P * fit_reps / fit_elapsed,
             "fit_ms": 1e3 * fit_elapsed / fit_reps,
-            # posterior update against the fp64 MFMA roofline at SURVEY §8d's n^3/3 flops (the Cholesky; the
-            # L^-T inverse computed for the sweep adds another n^3/3 not counted here): a latency-bound chain of
-            # n/64 dependent panel launches, far from the bound
+            "update_breakdown_ms": {"gram": part["gram"][0] / fit_reps, "potrf": part["potrf"][0] / fit_reps,
+                                    "alpha_potrs": part["alpha"][0] / fit_reps},
+            # posterior update (Gram + Cholesky + alpha by triangular solves; the L^-T a sweep needs is built by the
+            # sweep) against the fp64 MFMA roofline at SURVEY §8d's n^3/3 flops: a latency-bound chain of n/64
+            # dependent panel launches, far from the bound
             "updates_roofline": {"flops_per_update": n ** 3 / 3.0,
                                  "achieved": (n ** 3 / 3.0) * P / (fit_elapsed / fit_reps) / 1e12,
                                  "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -472,6 +495,12 @@ def main():
                                       "achieved": kstar_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                       "frac": kstar_gbs / HBM_PEAK_GBS, "bytes_per_launch": kstar_bytes,
                                       "avg_launch_ms": kstar_avg, "launches": kstar_launches},
+            # the training-set kernel build (gram_kernel) against HBM, as the north star asks: its algorithmic traffic
+            # is the write of the lower triangle of the padded K, 8 npad (npad + 1) / 2 bytes (+ X read once)
+            "gram_roofline": {"kernel": "gram_kernel (K(X, X) + noise I, lower triangle)", "bound": "hbm",
+                              "achieved": gram_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": gram_gbs / HBM_PEAK_GBS, "bytes_per_launch": gram_bytes,
+                              "avg_launch_ms": gram_avg, "launches": part["gram"][1]},
             "cpu_baseline": cpu,
             "other_configs": extra,
         }

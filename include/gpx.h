@@ -144,6 +144,13 @@ gpx_status gpx_trtri_workspace_size(int64_t n, size_t* bytes);
 gpx_status gpx_trtri_f64(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv, double* W,
                          int64_t ldw, void* ws, size_t ws_bytes);
 
+/* The same for `batch` factors at fixed element strides (the W of gpx_fit_factor_batched_f64's problems before their
+ * sweeps), in the same launches. */
+gpx_status gpx_trtri_batched_workspace_size(int64_t n, int64_t batch, size_t* bytes);
+gpx_status gpx_trtri_batched_f64(gpx_handle h, int64_t batch, int64_t n, const double* L, int64_t ldl, int64_t stride_l,
+                                 const double* Dinv, int64_t stride_dinv, double* W, int64_t ldw, int64_t stride_w,
+                                 void* ws, size_t ws_bytes);
+
 /* alpha = K^{-1} (Y - const_mean) = W W^T (Y - m) for nrhs <= GPX_MAX_RHS right-hand sides.  Y: n x nrhs
  * row-major with leading dim ldy; alpha: contiguous padded_n x nrhs (rows >= n are set to 0).
  * Replaces the ExactGP mean_cache [upstream]. */

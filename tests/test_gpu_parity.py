@@ -427,10 +427,10 @@ def test_fit_batched_matches_single_fits_and_oracle(engine, n, B, nrhs, inverse)
         Xs.append(X)
         Ys.append(np.stack([y * (r + 1) + r for r in range(nrhs)], axis=1))
     sts = engine.fit_batched(t(np.stack(Xs)), t(np.stack(Ys)), kp, inverse=inverse)
+    assert all(st.W_ready == inverse for st in sts)
+    engine.inverse_batched(sts)  # factor-only: every W in the same launches (gpx_trtri_batched_f64)
     for b in range(B):
         single = engine.fit(t(Xs[b]), t(Ys[b]), kp, inverse=inverse)
-        assert sts[b].W_ready == inverse
-        engine.inverse(sts[b])
         engine.inverse(single)
         # same kernels, same inputs: identical factor, inverse and alpha
         assert torch.equal(torch.tril(sts[b].L[:n, :n]), torch.tril(single.L[:n, :n]))
