@@ -8,10 +8,11 @@
 // one row of the tile at a time and writes 64 consecutive doubles (512 B) per store instruction.
 #include "gpx_internal.h"
 #include "gpx_device.h"
+#include <cstdlib>
 
 namespace gpx {
 
-template <int DMAX, bool F32>
+template <int DMAX, bool F32, int KIND>
 __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, int t0, const double* __restrict__ X,
                                                   int64_t ldx, double* __restrict__ K, int64_t ldk, int64_t sx,
                                                   int64_t sk, int32_t* __restrict__ info) {
@@ -26,7 +27,7 @@ __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, in
   tri_decode(t0 + (int)blockIdx.x, ti, tj);
   const int i0 = ti * NB, j0 = tj * NB;
   const int d = p.d;
-  const bool lin = (p.kind == GPX_KERNEL_SCALE_LINEAR_MATERN52);
+  constexpr bool lin = (KIND == GPX_KERNEL_SCALE_LINEAR_MATERN52);
   for (int e = threadIdx.x; e < NB * DMAX; e += WG) {
     int r = e / DMAX, k = e % DMAX;
     double xi = 0.0, xj = 0.0;
@@ -50,12 +51,18 @@ __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, in
     rc[k] = rj[c][k];
   }
   const double diag_add = p.noise + p.jitter;
-  // gridDim.z row slices per tile (small fits: more workgroups, fewer serial exp chains per thread)
+  // gridDim.z row slices per tile (small fits: more workgroups, fewer serial exp chains per thread).  The rows of a
+  // thread are processed four at a time (independent distance / exp chains in flight together: the one-row loop left
+  // the kernel at 0.24 of HBM, latency-bound on the fp64 exp chain); the covariance kind is a template parameter so
+  // the element loop has no uniform branches.
   const int rows = NB / gridDim.z, rbeg = blockIdx.z * rows;
-  for (int r = rbeg + (threadIdx.x >> 6); r < rbeg + rows; r += 4) {
-    const int gi = i0 + r;
-    double v;
-    if (gi < n && gj < n) {
+  const int rw = threadIdx.x >> 6;
+  for (int r0 = rbeg; r0 < rbeg + rows; r0 += 16) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int r = r0 + rw + 4 * u;
+      const int gi = i0 + r;
       double lv = 0.0;
       if (lin) {
 #pragma unroll
@@ -71,7 +78,7 @@ __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, in
             r2 += df * df;
           }
         }
-        v = cov_from_r2_f32(p.kind, p.outputscale, r2, lv);
+        v[u] = cov_from_r2_f32(KIND, p.outputscale, r2, lv);
       } else {
         double r2 = 0.0;
 #pragma unroll
@@ -81,13 +88,13 @@ __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, in
             r2 += df * df;
           }
         }
-        v = cov_from_r2(p.kind, p.outputscale, r2, lv);
+        v[u] = cov_from_r2(KIND, p.outputscale, r2, lv);
       }
-      if (gi == gj) v += diag_add;
-    } else {
-      v = (gi == gj) ? 1.0 : 0.0;  // identity padding
+      if (gi == gj) v[u] += diag_add;
+      if (gi >= n || gj >= n) v[u] = (gi == gj) ? 1.0 : 0.0;  // identity padding
     }
-    K[(int64_t)gi * ldk + gj] = v;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) K[(int64_t)(i0 + r0 + rw + 4 * u) * ldk + gj] = v[u];
   }
 }
 
@@ -97,11 +104,22 @@ hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, 
   const int nblk = npad / NB;
   const int t0 = rb0 * (rb0 + 1) / 2;  // tiles of the row blocks above rb0 are skipped (gpx_append_f64)
   const int tiles = (nblk * (nblk + 1) / 2 - t0) * bt.count;
-  // fewer tiles than CUs: split each tile's 64 rows over 4 workgroups (n = 128: 11 -> see DESIGN §5)
-  const dim3 grid(nblk * (nblk + 1) / 2 - t0, bt.count, tiles < 256 ? 4 : 1);
+  // fewer tiles than CUs: split each tile's 64 rows over 4 workgroups (n = 128: 11 -> see DESIGN §5); GPX_GRAM_SPLIT
+  // overrides (1, 2 or 4)
+  static const int split_env = [] {
+    const char* e = std::getenv("GPX_GRAM_SPLIT");
+    return e ? std::atoi(e) : 0;
+  }();
+  int split = tiles < 256 ? 4 : 1;
+  if (split_env == 1 || split_env == 2 || split_env == 4) split = split_env;
+  const dim3 grid(nblk * (nblk + 1) / 2 - t0, bt.count, split);
+#define GPX_GRAM_K(D, KIND)                                                                                      \
+  (p.cov_fp32 ? gram_kernel<D, true, KIND><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info) \
+              : gram_kernel<D, false, KIND><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info))
 #define GPX_GRAM(D)                                                                                              \
-  (p.cov_fp32 ? gram_kernel<D, true><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info) \
-              : gram_kernel<D, false><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info))
+  (p.kind == GPX_KERNEL_RBF        ? GPX_GRAM_K(D, GPX_KERNEL_RBF)                                               \
+   : p.kind == GPX_KERNEL_MATERN52 ? GPX_GRAM_K(D, GPX_KERNEL_MATERN52)                                          \
+                                   : GPX_GRAM_K(D, GPX_KERNEL_SCALE_LINEAR_MATERN52))
   if (p.d <= 4)
     GPX_GRAM(4);
   else if (p.d <= 8)
@@ -111,6 +129,7 @@ hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, 
   else
     GPX_GRAM(32);
 #undef GPX_GRAM
+#undef GPX_GRAM_K
   return hipGetLastError();
 }
 

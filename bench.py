@@ -312,6 +312,50 @@ def other_configs(eng, dev, seed):
         "acq_cands_per_s": P4 * (1 << 20) / t, "best_index": int(bi.item())}
     del sts, Xb, yb, Xs4
     torch.cuda.empty_cache()
+    # the driven variant (Bayesian7) at its own configuration: T = 8 tasks, M = 2048 inducing points
+    # (random-init variational state of that shape), d = 5; a 10,000-candidate pool scan (score -> top 8000 -> FPS of
+    # 500, optimization/Bayesian7.py:646-688) and the predictive's scoring rate on 2^20 candidates
+    from bayesianoptimizer_amd.svgp import SVGPModel, SVGPPredictor
+    rng = np.random.default_rng(seed + 19)
+    T8, M8, d5 = 8, 2048, 5
+    Z = rng.standard_normal((T8, M8, d5))
+    vchol = np.tril(0.3 * rng.standard_normal((T8, M8, M8)) / np.sqrt(M8))
+    for t in range(T8):
+        vchol[t][np.diag_indices(M8)] = 0.2 + 0.5 * rng.random(M8)
+    kps = [KernelParams("scale_linear_matern52", list(0.8 + rng.random(d5)), outputscale=0.5 + rng.random(),
+                        noise=1e-3, const_mean=0.0, linear_variance=list(0.05 + 0.1 * rng.random(d5)))
+           for _ in range(T8)]
+    model = SVGPModel(Z=torch.tensor(Z), vmean=torch.tensor(rng.standard_normal((T8, M8))),
+                      vchol=torch.tensor(vchol), params=kps)
+    torch.cuda.synchronize()
+    a = time.perf_counter()
+    pred = SVGPPredictor(model, eng)
+    torch.cuda.synchronize()
+    t_prep = time.perf_counter() - a
+    pool = torch.tensor(rng.random((10000, d5)), device=dev)
+    big = torch.tensor(rng.random((1 << 20, d5)), device=dev)
+    pred.pool_scan(pool, batch_k=500, start=0)
+    pred.uncertainty(big, transformed=True)
+    tp, tb = [], []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        pred.pool_scan(pool, batch_k=500, start=0)
+        torch.cuda.synchronize()
+        b = time.perf_counter()
+        pred.uncertainty(big, transformed=True)
+        torch.cuda.synchronize()
+        tp.append(b - a)
+        tb.append(time.perf_counter() - b)
+    out["svgp driven config (Bayesian7)"] = {
+        "workload": "batched SVGP predictive, T=8 tasks, M=2048 inducing points, d=5 (ScaleKernel(Linear+Matern-5/2) "
+                    "per task): 10,000-candidate pool scan (variance-sum score, top 8000, FPS of 500) and the "
+                    "score of 1048576 candidates",
+        "prepare_ms": 1e3 * t_prep, "pool_scan_ms": 1e3 * float(np.median(tp)),
+        "score_cands_per_s": (1 << 20) / float(np.median(tb)),
+        "score_tflops_3M2_per_cand_task": 3.0 * M8 * M8 * T8 * (1 << 20) / float(np.median(tb)) / 1e12}
+    del pred, model, pool, big
+    torch.cuda.empty_cache()
     # the BO loop's per-iteration update done incrementally: one new observation appended to an
     # n = 4096 fit by the bordered Cholesky (gpx_append_f64; the same factor a refit computes, GPU parity tests),
     # beside the headline's full refit

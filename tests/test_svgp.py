@@ -149,3 +149,29 @@ def test_pool_scan_end_to_end(engine):
     sel = O.farthest_point_sampling(cand[big], 300, 42)
     np.testing.assert_array_equal(idx.cpu().numpy(), big[sel])
     np.testing.assert_array_equal(pts.cpu().numpy(), cand[big[sel]])
+
+
+@pytest.mark.gpu
+def test_svgp_driven_config_T8_M2048_pool_scan(engine):
+    """The configuration Bayesian7 actually runs (/root/reference/optimization/Bayesian7.py:32,45,57,63,138): T = 8
+    tasks, M = 2048 inducing points, a 10,000-candidate LHS pool scored in 2048-row chunks, top K_big = 8000 by the
+    variance sum, then farthest-point sampling of acq_batch_size = 500.  Predictive mean / variance / score against the
+    oracle at 1e-9 and the selected pool indices bit-exact against the oracle's top-k + FPS on the oracle's scores."""
+    from bayesianoptimizer_amd.svgp import SVGPPredictor
+
+    T, M, d, m, batch_k = 8, 2048, 5, 10000, 500
+    Z, vmean, vchol, kps, ops = svgp_problem(T, M, d, seed=2048)
+    cand = np.random.default_rng(6).random((m, d))
+    model = SVGPModel(Z=torch.tensor(Z), vmean=torch.tensor(vmean), vchol=torch.tensor(vchol), params=kps)
+    pred = SVGPPredictor(model, engine)
+    mu, var, score = engine.svgp_predict(pred.prep, torch.tensor(cand, device=engine.device))
+    mu_r, var_r, score_r = O.svgp_predict(Z, vmean, vchol, ops, cand)
+    mu, var, score = mu.cpu().numpy(), var.cpu().numpy(), score.cpu().numpy()
+    assert np.abs(mu - mu_r).max() <= 1e-9 * np.abs(mu_r).max()
+    assert np.abs(var - var_r).max() <= 1e-9 * np.abs(var_r).max()
+    assert np.abs(score - score_r).max() <= 1e-9 * np.abs(score_r).max()
+    pts, idx = pred.pool_scan(torch.tensor(cand), batch_k=batch_k, start=123)
+    k_big = min(max(5000, 20 * batch_k), 8000, m)
+    _, big = O.topk_desc(score_r, k_big)
+    sel = O.farthest_point_sampling(cand[big], batch_k, 123)
+    np.testing.assert_array_equal(idx.cpu().numpy(), big[sel])
