@@ -164,7 +164,14 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
     const int o = 16 * s;
     double* D = sDb + (s & 1) * 16 * LDD;
     if (w == 0) {
+#ifndef GPX_CHOL16_MFMA
       const int f = chol16<LDD>(sA, D, o);
+#else
+      // 4-pivot blocks on v_mfma_f64_16x16x4 (gpx_chol64.h): correct, but measured slower inside the panel (potrf
+      // 1.89 vs 1.76 ms at n = 4096): like the rank-1 form it issues ~75 instructions per pivot (selects of the
+      // uniform 4x4 factors, cross-row broadcasts) and exposes MFMA / ds_bpermute latency on the chain
+      const int f = chol16_mfma<LDD>(sA, D, o);
+#endif
       if (f >= 0 && fail < 0) fail = o + f;
     }
     GPX_PANEL_STAMP(1 + 3 * s);

@@ -76,6 +76,10 @@ class KernelParams:
     linear_variance: Optional[np.ndarray] = None
     jitter: float = 0.0
     cov_fp32: bool = False  # BASELINE configs[4]: covariance evaluated in fp32, widened before factorisation
+    # "difference": sum_k ((a_k - b_k)/l_k)^2, the form the GPU kernels compute; "expanded": GPyTorch's
+    # ||a||^2 + ||b||^2 - 2 a.b on inputs centred by mean(X1), clamped >= 0, diagonal zeroed for K(X, X) [upstream]
+    # (used only to bound the formulation gap to GPyTorch, tests/test_oracle.py)
+    dist_form: str = "difference"
 
     def __post_init__(self):
         self.lengthscale = np.asarray(self.lengthscale, dtype=np.float64).reshape(-1)
@@ -111,13 +115,31 @@ def _sqdist_scaled(X1: np.ndarray, X2: np.ndarray, ls: np.ndarray) -> np.ndarray
     return out
 
 
+def _sqdist_scaled_expanded(X1: np.ndarray, X2: np.ndarray, ls: np.ndarray, same: bool) -> np.ndarray:
+    """GPyTorch's Distance._sq_dist [upstream] restated: scale by the lengthscales, centre both inputs by mean(X1),
+    r2 = ||a||^2 + ||b||^2 - 2 a.b, clamped at 0, the diagonal set to 0 when X1 is X2."""
+    A = X1 / ls
+    B = X2 / ls
+    adj = A.mean(axis=0, keepdims=True)
+    A = A - adj
+    B = B - adj
+    r2 = (A * A).sum(1)[:, None] + (B * B).sum(1)[None, :] - 2.0 * (A @ B.T)
+    if same:
+        np.fill_diagonal(r2, 0.0)
+    return np.maximum(r2, 0.0)
+
+
 def kernel_matrix(X1: np.ndarray, X2: np.ndarray, p: KernelParams) -> np.ndarray:
     """k(X1, X2) without noise.  Formulas per GPyTorch RBFKernel/MaternKernel/LinearKernel/ScaleKernel."""
+    same = X1 is X2
     X1 = np.asarray(X1, dtype=np.float64)
     X2 = np.asarray(X2, dtype=np.float64)
     if p.cov_fp32:
         return _kernel_matrix_f32(X1, X2, p)
-    r2 = _sqdist_scaled(X1, X2, p.lengthscale)
+    if p.dist_form == "expanded":
+        r2 = _sqdist_scaled_expanded(X1, X2, p.lengthscale, same)
+    else:
+        r2 = _sqdist_scaled(X1, X2, p.lengthscale)
     if p.kind == RBF:
         return p.outputscale * np.exp(-0.5 * r2)
     r = np.sqrt(r2)

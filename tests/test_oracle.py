@@ -188,3 +188,24 @@ def test_append_not_pd_global_pivot():
     with pytest.raises(O.NotPDError) as e:
         O.append(st, X, np.zeros(32))
     assert e.value.pivot == 31
+
+
+@pytest.mark.parametrize("kind,n,d,noise", [(O.RBF, 600, 8, 1e-4), (O.MATERN52, 600, 8, 1e-4), (O.RBF, 400, 4, 1e-6)])
+def test_distance_form_gap_to_gpytorch_is_below_the_parity_tolerance(kind, n, d, noise):
+    """The GPU kernels evaluate distances in the difference form sum_k ((a_k - b_k)/l_k)^2; GPyTorch [upstream] uses
+    ||a||^2 + ||b||^2 - 2 a.b on mean-centred inputs.  Both are restated in the oracle (KernelParams.dist_form); this
+    bounds how far the two formulations' posteriors drift apart on the north star's inputs, so that the 1e-9 parity
+    tolerance against the oracle also bounds the distance to GPyTorch's arithmetic."""
+    X, y = O.synthetic_problem(n, d, 5)
+    ls = np.full(d, O.botorch_default_lengthscale(d))
+    pd = O.KernelParams(kind, ls, noise=noise)
+    pe = O.KernelParams(kind, ls, noise=noise, dist_form="expanded")
+    Kd, Ke = O.gram(X, pd), O.gram(X, pe)
+    assert np.abs(Kd - Ke).max() <= 1e-14  # O(eps) per entry
+    Xs = O.sobol_candidates(500, d, 6)
+    mu_d, var_d = O.posterior(O.fit(X, y, pd), Xs)
+    mu_e, var_e = O.posterior(O.fit(X, y, pe), Xs)
+    dmu = np.abs(mu_d - mu_e).max() / np.abs(mu_d).max()
+    dvar = np.abs(var_d - var_e).max()
+    assert dmu <= 1e-10, dmu
+    assert dvar <= 1e-10, dvar
