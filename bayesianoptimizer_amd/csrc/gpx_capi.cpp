@@ -170,7 +170,7 @@ const char* gpx_last_error(gpx_handle h) {
 
 // gram_impl clears *info (when given) inside the gram kernel: the fit needs no separate memset dispatch
 static gpx_status gram_impl(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
-                            double* K, int64_t ldk, int32_t* info) {
+                            double* K, int64_t ldk, int32_t* info, void* zero = nullptr, size_t zero_bytes = 0) {
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return GPX_INVALID_ARG;
   GPX_TRY(check_params(c, p));
@@ -181,7 +181,8 @@ static gpx_status gram_impl(gpx_handle h, const gpx_kernel_params* p, int64_t n,
   GPX_TRY(check_ld(c, ldx, p->d, "X", false));
   GPX_TRY(check_ld(c, ldk, npad, "K", true));
   GPX_USE_DEVICE(c);
-  return hip_check(c, gpx::launch_gram(c, *p, (int)n, (int)npad, X, ldx, K, ldk, gpx::Batch(), 0, info), "gram");
+  return hip_check(c, gpx::launch_gram(c, *p, (int)n, (int)npad, X, ldx, K, ldk, gpx::Batch(), 0, info, zero, zero_bytes),
+                   "gram");
 }
 
 gpx_status gpx_gram_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
@@ -351,9 +352,19 @@ gpx_status gpx_potrs_workspace_size(int64_t n, int64_t nrhs, size_t* bytes) {
   return GPX_OK;
 }
 
+static gpx_status potrs_impl(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv,
+                             const double* Y, int64_t ldy, int64_t nrhs, double const_mean, double* alpha,
+                             const int32_t* info, void* ws, size_t ws_bytes, bool ws_cleared);
+
 gpx_status gpx_potrs_f64(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv, const double* Y,
                          int64_t ldy, int64_t nrhs, double const_mean, double* alpha, const int32_t* info, void* ws,
                          size_t ws_bytes) {
+  return potrs_impl(h, n, L, ldl, Dinv, Y, ldy, nrhs, const_mean, alpha, info, ws, ws_bytes, false);
+}
+
+static gpx_status potrs_impl(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv,
+                             const double* Y, int64_t ldy, int64_t nrhs, double const_mean, double* alpha,
+                             const int32_t* info, void* ws, size_t ws_bytes, bool ws_cleared) {
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return GPX_INVALID_ARG;
   GPX_TRY(check_n(c, n));
@@ -371,7 +382,7 @@ gpx_status gpx_potrs_f64(gpx_handle h, int64_t n, const double* L, int64_t ldl, 
   if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "potrs workspace too small");
   GPX_USE_DEVICE(c);
   return hip_check(c, gpx::launch_potrs(c, (int)n, (int)npad, L, ldl, Dinv, Y, ldy, (int)nrhs, const_mean, alpha, info,
-                                        align256(ws)),
+                                        align256(ws), gpx::Batch(), ws_cleared),
                    "potrs");
 }
 
@@ -389,9 +400,11 @@ gpx_status gpx_fit_factor_f64(gpx_handle h, const gpx_kernel_params* p, int64_t 
     return fail(c, GPX_INVALID_ARG, "invalid n / nrhs for fit");
   if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "fit workspace too small");
   if (!info) return fail(c, GPX_INVALID_ARG, "info is NULL");
-  GPX_TRY(gram_impl(h, p, n, X, ldx, K, ldk, info));
+  if (!ws) return fail(c, GPX_INVALID_ARG, "ws is NULL");
+  // the Gram launch also clears the triangular solve's hand-off granules (no memset dispatch)
+  GPX_TRY(gram_impl(h, p, n, X, ldx, K, ldk, info, align256(ws), gpx::potrs_clear_bytes(padded(n), nrhs, 1)));
   GPX_TRY(potrf_impl(h, n, K, ldk, Dinv, info, false));
-  return gpx_potrs_f64(h, n, K, ldk, Dinv, Y, ldy, nrhs, p->const_mean, alpha, info, ws, ws_bytes);
+  return potrs_impl(h, n, K, ldk, Dinv, Y, ldy, nrhs, p->const_mean, alpha, info, ws, ws_bytes, true);
 }
 
 gpx_status gpx_append_workspace_size(int64_t n_old, int64_t n_new, int64_t nrhs, size_t* bytes) {
@@ -502,11 +515,15 @@ static gpx_status fit_batched_impl(gpx_handle h, const gpx_kernel_params* p, int
   bt.ws = (int64_t)(fit_slice_bytes(npad, nrhs) / sizeof(double));
   double* slice = align256(ws);
   // the gram kernel clears info[0 .. batch) before the Cholesky (no separate memset dispatch)
-  GPX_TRY(hip_check(c, gpx::launch_gram(c, *p, (int)n, (int)npad, X, ldx, K, ldk, bt, 0, info), "gram"));
+  // the Gram launch also clears the triangular solve's hand-off granules of a factor-only fit (no memset dispatch)
+  GPX_TRY(hip_check(c, gpx::launch_gram(c, *p, (int)n, (int)npad, X, ldx, K, ldk, bt, 0, info,
+                                        inverse ? nullptr : slice,
+                                        inverse ? 0 : gpx::potrs_clear_bytes(npad, nrhs, batch)),
+                    "gram"));
   GPX_TRY(hip_check(c, gpx::launch_potrf(c, (int)npad, K, ldk, Dinv, info, bt, W, ldw), "potrf"));
   if (!inverse)
     return hip_check(c, gpx::launch_potrs(c, (int)n, (int)npad, K, ldk, Dinv, Y, ldy, (int)nrhs, p->const_mean, alpha,
-                                          info, slice, bt),
+                                          info, slice, bt, true),
                      "potrs");
   GPX_TRY(hip_check(c, gpx::launch_trtri(c, (int)npad, K, ldk, Dinv, W, ldw, slice, bt, true), "trtri"));
   double* zpart = slice;

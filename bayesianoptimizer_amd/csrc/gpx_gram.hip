@@ -15,10 +15,17 @@ namespace gpx {
 template <int DMAX, bool F32, int KIND>
 __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, int t0, const double* __restrict__ X,
                                                   int64_t ldx, double* __restrict__ K, int64_t ldk, int64_t sx,
-                                                  int64_t sk, int32_t* __restrict__ info) {
+                                                  int64_t sk, int32_t* __restrict__ info,
+                                                  unsigned long long* __restrict__ zero, int64_t zero_words) {
   // the fit's pivot-failure word is cleared here (stream-ordered before the Cholesky) instead of by a separate
-  // memset dispatch (~4.7 us at small n)
+  // memset dispatch (~4.7 us at small n), and so are the words of `zero` (the triangular solve's hand-off granules,
+  // gpx_fit_factor_f64): one more dispatch saved
   if (info && blockIdx.x == 0 && blockIdx.z == 0 && threadIdx.x == 0) info[blockIdx.y] = 0;
+  if (zero) {
+    const int64_t nwg = (int64_t)gridDim.x * gridDim.y * gridDim.z;
+    const int64_t wg = blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z);
+    for (int64_t e = wg * WG + threadIdx.x; e < zero_words; e += nwg * WG) zero[e] = 0ull;
+  }
   X += blockIdx.y * sx;  // problem of a batched fit
   K += blockIdx.y * sk;
   __shared__ double si[NB][DMAX + 1], sj[NB][DMAX + 1];    // scaled x / l
@@ -99,7 +106,8 @@ __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, in
 }
 
 hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
-                       double* K, int64_t ldk, const Batch& bt, int rb0, int32_t* info) {
+                       double* K, int64_t ldk, const Batch& bt, int rb0, int32_t* info, void* zero,
+                       size_t zero_bytes) {
   LaunchTimer tm(c, GPX_TIMER_GRAM);
   const int nblk = npad / NB;
   const int t0 = rb0 * (rb0 + 1) / 2;  // tiles of the row blocks above rb0 are skipped (gpx_append_f64)
@@ -113,9 +121,11 @@ hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, 
   int split = tiles < 256 ? 4 : 1;
   if (split_env == 1 || split_env == 2 || split_env == 4) split = split_env;
   const dim3 grid(nblk * (nblk + 1) / 2 - t0, bt.count, split);
+  auto* zp = reinterpret_cast<unsigned long long*>(zero);
+  const int64_t zw = zero ? (int64_t)(zero_bytes / 8) : 0;
 #define GPX_GRAM_K(D, KIND)                                                                                      \
-  (p.cov_fp32 ? gram_kernel<D, true, KIND><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info) \
-              : gram_kernel<D, false, KIND><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info))
+  (p.cov_fp32 ? gram_kernel<D, true, KIND><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info, zp, zw) \
+              : gram_kernel<D, false, KIND><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info, zp, zw))
 #define GPX_GRAM(D)                                                                                              \
   (p.kind == GPX_KERNEL_RBF        ? GPX_GRAM_K(D, GPX_KERNEL_RBF)                                               \
    : p.kind == GPX_KERNEL_MATERN52 ? GPX_GRAM_K(D, GPX_KERNEL_MATERN52)                                          \

@@ -73,8 +73,10 @@ struct Batch {
 };
 
 // ---- launch wrappers (defined in the .hip files) -------------------------------------------------
+// zero / zero_bytes (optional, a multiple of 8): a buffer the Gram launch clears besides (the next launches' flags)
 hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
-                       double* K, int64_t ldk, const Batch& bt = Batch(), int rb0 = 0, int32_t* info = nullptr);
+                       double* K, int64_t ldk, const Batch& bt = Batch(), int rb0 = 0, int32_t* info = nullptr,
+                       void* zero = nullptr, size_t zero_bytes = 0);
 // W (optional): the Dinv pass also writes W's diagonal blocks D_k^T (what trtri_diag would), so a fit that follows
 // with launch_trtri(..., diag_done = true) saves one dispatch.
 hipError_t launch_potrf(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info,
@@ -87,9 +89,11 @@ hipError_t launch_alpha(Context* c, int n, int npad, const double* W, int64_t ld
 // alpha from L + Dinv by forward/backward triangular solves (gpx_potrs.hip); ws: potrs_workspace_bytes, zeroed by
 // the launch itself (its hand-off granules)
 size_t potrs_workspace_bytes(int64_t npad, int64_t nrhs, int64_t batch);
+// ws_cleared: the granule block (potrs_clear_bytes) was already zeroed on the stream (by launch_gram in a fit)
+size_t potrs_clear_bytes(int64_t npad, int64_t nrhs, int64_t batch);
 hipError_t launch_potrs(Context* c, int n, int npad, const double* L, int64_t ldl, const double* Dinv,
                         const double* Y, int64_t ldy, int nrhs, double const_mean, double* alpha,
-                        const int32_t* info, void* ws, const Batch& bt = Batch());
+                        const int32_t* info, void* ws, const Batch& bt = Batch(), bool ws_cleared = false);
 
 struct SweepBuffers {
   double* kstar;     // npad x C

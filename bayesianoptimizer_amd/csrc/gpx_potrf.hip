@@ -512,7 +512,7 @@ __host__ __device__ inline StepPlan step_plan(int c, int nblk, int lazy, int mod
 
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
 potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, int lazy, int mode, double* __restrict__ Dinv,
-                  int32_t* __restrict__ info, int first_wg, int64_t sa, int64_t sd) {
+                  int32_t* __restrict__ info, int first_wg, int64_t sa, int64_t sd, int prio) {
   A += blockIdx.y * sa;  // problem of a batched fit
   Dinv += blockIdx.y * sd;
   info += blockIdx.y;
@@ -520,6 +520,8 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, int lazy
   __shared__ __attribute__((aligned(16))) double lds[STEP_LDS];
   const StepPlan s = step_plan(c, nblk, lazy, mode);
   const int b = first_wg + (int)blockIdx.x;
+  // the panel is the launch's critical path; its waves share SIMDs with trailing tiles' MFMA streams
+  if (prio && b < s.npanel) __builtin_amdgcn_s_setprio(3);
   if (b < s.npanel)
     panel_role(A, lda, c, b, nblk, s.c0, Dinv, info, lds);
   else if (b < s.npanel + s.nlook)
@@ -604,9 +606,11 @@ int potrf_step_grid(int c, int nblk, int lazy, int mode) {
 static void launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
                          int cbeg, int cend) {
   const int lazy = potrf_lazy(nblk), mode = potrf_mode(nblk);
+  static const int prio_env = env_int("GPX_POTRF_PRIO");
+  const int prio = prio_env < 0 ? 0 : prio_env;
   for (int c = cbeg; c < cend; ++c)
     potrf_step_kernel<<<dim3(potrf_step_grid(c, nblk, lazy, mode), bt.count), WG, 0, ctx->stream>>>(
-        A, lda, c, nblk, lazy, mode, Dinv, info, 0, bt.k, bt.dinv);
+        A, lda, c, nblk, lazy, mode, Dinv, info, 0, bt.k, bt.dinv, prio);
 }
 
 static void launch_dinv(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,

@@ -600,18 +600,24 @@ size_t potrs_granule_bytes(int64_t npad, int64_t nrhs) {
   return (size_t)(2 * npad * nr * 2) * sizeof(unsigned long long);
 }
 
+size_t potrs_clear_bytes(int64_t npad, int64_t nrhs, int64_t batch) {
+  return ((potrs_granule_bytes(npad, nrhs) * batch + 4 * (size_t)batch) + 15) & ~(size_t)15;
+}
+
 hipError_t launch_potrs(Context* c, int n, int npad, const double* L, int64_t ldl, const double* Dinv,
                         const double* Y, int64_t ldy, int nrhs, double const_mean, double* alpha,
-                        const int32_t* info, void* ws, const Batch& bt) {
+                        const int32_t* info, void* ws, const Batch& bt, bool ws_cleared) {
   LaunchTimer tm(c, GPX_TIMER_ALPHA);
   const int nb = npad / SB;
-  // granules of every problem, then one abort word per problem; zeroed as ONE block from the workspace start
+  // granules of every problem, then one abort word per problem; zeroed as ONE block from the workspace start (by the
+  // fit's Gram launch, or here)
   const size_t gbytes = potrs_granule_bytes(npad, nrhs);
   auto* granules = reinterpret_cast<unsigned long long*>(ws);
   auto* abort_word = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(ws) + gbytes * bt.count);
-  const size_t clear = ((gbytes * bt.count + 4 * (size_t)bt.count) + 15) & ~(size_t)15;
-  hipError_t e = hipMemsetAsync(ws, 0, clear, c->stream);
-  if (e != hipSuccess) return e;
+  if (!ws_cleared) {
+    hipError_t e = hipMemsetAsync(ws, 0, potrs_clear_bytes(npad, nrhs, bt.count), c->stream);
+    if (e != hipSuccess) return e;
+  }
   // co-resident grid (one 124 KB workgroup per CU at NR = 8): at most 256 workgroups in all
   int G = 256 / bt.count;
   if (G < 1) G = 1;
@@ -629,7 +635,7 @@ hipError_t launch_potrs(Context* c, int n, int npad, const double* L, int64_t ld
 }
 
 size_t potrs_workspace_bytes(int64_t npad, int64_t nrhs, int64_t batch) {
-  return potrs_granule_bytes(npad, nrhs) * batch + 4 * batch + 64;
+  return potrs_clear_bytes(npad, nrhs, batch) + 64;
 }
 
 }  // namespace gpx
