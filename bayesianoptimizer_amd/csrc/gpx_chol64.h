@@ -101,9 +101,59 @@ __device__ __forceinline__ void chol16_pivot(Blk16& b, int r, int g, int& fail) 
   }
 }
 
+// a[q] += ca * bcast_J(a[q]) and x[q] += cx * bcast_J(x[q]) (q = 0..3) as eight v_fmac_f64_dpp row_newbcast:J: the
+// gfx90a+ 64-bit DPP form folds the row broadcast into the FMA (hipcc emits v_mov_b64_dpp + v_fmac_f64 instead, three
+// instructions per value with the 32-bit halves).  The compiler's hazard recognizer does not see inside the asm, so
+// the block pads the DPP read of a fresh VALU result and the next DPP / permlane read of its outputs (2 wait states
+// each, as hipcc pads its own).
+#define GPX_FMAC_DPP8(J)                                                                                         \
+  case J:                                                                                                        \
+    asm("s_nop 1\n\t"                                                                                            \
+        "v_fmac_f64_dpp %0, %0, %8 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                           \
+        "v_fmac_f64_dpp %1, %1, %8 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                           \
+        "v_fmac_f64_dpp %2, %2, %8 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                           \
+        "v_fmac_f64_dpp %3, %3, %8 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                           \
+        "v_fmac_f64_dpp %4, %4, %9 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                           \
+        "v_fmac_f64_dpp %5, %5, %9 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                           \
+        "v_fmac_f64_dpp %6, %6, %9 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                           \
+        "v_fmac_f64_dpp %7, %7, %9 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                           \
+        "s_nop 1"                                                                                                \
+        : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3])         \
+        : "v"(ca), "v"(cx));                                                                                     \
+    break;
+template <int J>
+__device__ __forceinline__ void fmac_row_bcast8(double (&a)[4], double (&x)[4], double ca, double cx) {
+  switch (J) {
+    GPX_FMAC_DPP8(0) GPX_FMAC_DPP8(1) GPX_FMAC_DPP8(2) GPX_FMAC_DPP8(3) GPX_FMAC_DPP8(4) GPX_FMAC_DPP8(5)
+    GPX_FMAC_DPP8(6) GPX_FMAC_DPP8(7) GPX_FMAC_DPP8(8) GPX_FMAC_DPP8(9) GPX_FMAC_DPP8(10) GPX_FMAC_DPP8(11)
+    GPX_FMAC_DPP8(12) GPX_FMAC_DPP8(13) GPX_FMAC_DPP8(14) GPX_FMAC_DPP8(15)
+  }
+}
+#undef GPX_FMAC_DPP8
+
+// chol16_pivot with the row broadcasts folded into the FMAs (fmac_row_bcast8): same arithmetic, same rounding (the
+// broadcast value is the pre-update A[J][c] / X[J][c], as in chol16_pivot).
+template <int J>
+__device__ __forceinline__ void chol16_pivot_fused(Blk16& b, int r, int g, int& fail) {
+  constexpr int GJ = J >> 2, QJ = J & 3;
+  const double piv = readlane_f64(b.a[QJ], J + 16 * GJ);
+  const double arj = xrow_bcast_f64<GJ>(b.a[QJ]);  // A[r][J]
+  if (!(piv > 0.0) && fail < 0) fail = J;
+  const double isq = pivot_rsq(piv);
+  const double rinv = isq * isq;
+  const double coef = (r > J) ? -arj * rinv : 0.0;
+  const double coefx = (r == J) ? isq - 1.0 : coef;
+  if (g == GJ) b.l[QJ] = (r >= J) ? b.a[QJ] * isq : 0.0;
+  fmac_row_bcast8<J>(b.a, b.x, coef, coefx);
+}
+
 template <int... J>
 __device__ __forceinline__ void chol16_pivots(Blk16& b, int r, int g, int& fail, std::integer_sequence<int, J...>) {
+#ifndef GPX_CHOL16_UNFUSED
+  (chol16_pivot_fused<J>(b, r, g, fail), ...);
+#else
   (chol16_pivot<J>(b, r, g, fail), ...);
+#endif
 }
 
 // Factor + invert the 16x16 SPD block at (o, o) of the LDS tile sA (both triangles present, symmetric) with one
@@ -164,66 +214,81 @@ __device__ __forceinline__ double sel4(int i, double v0, double v1, double v2, d
   return i == 0 ? v0 : (i == 1 ? v1 : (i == 2 ? v2 : v3));
 }
 
+// sF: per step k, 32 doubles of wave-private LDS: L_kk then D_k = L_kk^{-1}, each 4x4 row-major (zeros above the
+// diagonal).  Lanes fetch their lane-dependent coefficients from it (one ds_read_b128 pair) instead of selecting
+// among the uniform values (v_cndmask chains were ~15 % of the first version's instructions).
 template <int K>
-__device__ __forceinline__ void chol16_block_step(d4& A, d4& X, int g, int col, int& fail) {
-  // 1. the 4x4 diagonal block, uniform
+__device__ __forceinline__ void chol16_block_step(d4& A, d4& X, int g, int col, unsigned& bad, double* sF) {
+  const int lane = threadIdx.x & 63;
+  // 1. the 4x4 diagonal block, uniform (v_readlane into SGPRs)
   const double a00 = readlane_f64(A[K], 4 * K), a10 = readlane_f64(A[K], 16 + 4 * K),
                a11 = readlane_f64(A[K], 16 + 4 * K + 1), a20 = readlane_f64(A[K], 32 + 4 * K),
                a21 = readlane_f64(A[K], 32 + 4 * K + 1), a22 = readlane_f64(A[K], 32 + 4 * K + 2),
                a30 = readlane_f64(A[K], 48 + 4 * K), a31 = readlane_f64(A[K], 48 + 4 * K + 1),
                a32 = readlane_f64(A[K], 48 + 4 * K + 2), a33 = readlane_f64(A[K], 48 + 4 * K + 3);
-  if (!(a00 > 0.0) && fail < 0) fail = 4 * K;
   const double r0 = pivot_rsq(a00);
   const double l00 = a00 * r0, l10 = a10 * r0, l20 = a20 * r0, l30 = a30 * r0;
   const double p1 = fma(-l10, l10, a11);
-  if (!(p1 > 0.0) && fail < 0) fail = 4 * K + 1;
   const double r1 = pivot_rsq(p1);
   const double l11 = p1 * r1, l21 = fma(-l20, l10, a21) * r1, l31 = fma(-l30, l10, a31) * r1;
   const double p2 = fma(-l21, l21, fma(-l20, l20, a22));
-  if (!(p2 > 0.0) && fail < 0) fail = 4 * K + 2;
   const double r2 = pivot_rsq(p2);
   const double l22 = p2 * r2, l32 = fma(-l31, l21, fma(-l30, l20, a32)) * r2;
   const double p3 = fma(-l32, l32, fma(-l31, l31, fma(-l30, l30, a33)));
-  if (!(p3 > 0.0) && fail < 0) fail = 4 * K + 3;
   const double r3 = pivot_rsq(p3);
   const double l33 = p3 * r3;
+  // failed pivots as bits 4k + i (branch-free: the values are uniform but the compiler cannot prove it)
+  bad |= ((a00 > 0.0) ? 0u : 1u) << (4 * K) | ((p1 > 0.0) ? 0u : 2u) << (4 * K) | ((p2 > 0.0) ? 0u : 4u) << (4 * K) |
+         ((p3 > 0.0) ? 0u : 8u) << (4 * K);
   // D_k = L_kk^{-1} (lower)
-  const double d00 = r0, d11 = r1, d22 = r2, d33 = r3;
-  const double d10 = -(l10 * d00) * d11, d21 = -(l21 * d11) * d22, d32 = -(l32 * d22) * d33;
-  const double d20 = -fma(l21, d10, l20 * d00) * d22;
-  const double d31 = -fma(l32, d21, l31 * d11) * d33;
-  const double d30 = -fma(l32, d20, fma(l31, d10, l30 * d00)) * d33;
-  // 2. X block row k <- D_k X_k: lane (g, c) needs X[4k+m][c] from lane (c, m) (same column, row group m)
-  {
-    const double x0 = xrow_bcast_f64<0>(X[K]), x1 = xrow_bcast_f64<1>(X[K]), x2 = xrow_bcast_f64<2>(X[K]),
-                 x3 = xrow_bcast_f64<3>(X[K]);
-    const double c0 = sel4(g, d00, d10, d20, d30), c1 = sel4(g, 0.0, d11, d21, d31), c2 = sel4(g, 0.0, 0.0, d22, d32),
-                 c3 = sel4(g, 0.0, 0.0, 0.0, d33);
-    X[K] = fma(c3, x3, fma(c2, x2, fma(c1, x1, c0 * x0)));
+  const double d10 = -(l10 * r0) * r1, d21 = -(l21 * r1) * r2, d32 = -(l32 * r2) * r3;
+  const double d20 = -fma(l21, d10, l20 * r0) * r2;
+  const double d31 = -fma(l32, d21, l31 * r1) * r3;
+  const double d30 = -fma(l32, d20, fma(l31, d10, l30 * r0)) * r3;
+  double* F = sF + 32 * K;
+  if (lane == 0) {
+    double2* F2 = reinterpret_cast<double2*>(F);
+    F2[0] = make_double2(l00, 0.0);
+    F2[1] = make_double2(0.0, 0.0);
+    F2[2] = make_double2(l10, l11);
+    F2[3] = make_double2(0.0, 0.0);
+    F2[4] = make_double2(l20, l21);
+    F2[5] = make_double2(l22, 0.0);
+    F2[6] = make_double2(l30, l31);
+    F2[7] = make_double2(l32, l33);
+    F2[8] = make_double2(r0, 0.0);
+    F2[9] = make_double2(0.0, 0.0);
+    F2[10] = make_double2(d10, r1);
+    F2[11] = make_double2(0.0, 0.0);
+    F2[12] = make_double2(d20, d21);
+    F2[13] = make_double2(r2, 0.0);
+    F2[14] = make_double2(d30, d31);
+    F2[15] = make_double2(d32, r3);
   }
-  // the factored block row k: L_kk on the diagonal block (lanes col in block k), 0 right of it
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): lane 0's table writes land before the wave reads them
+  const double* Dk = F + 16;
+  const int m = lane & 15, kk = lane >> 4;  // MFMA A/B operand coordinates of this lane
+  // 2. X block row k <- D_k X_k as one MFMA: A = D_k in rows 4k..4k+3 (lane (kk, m): D_k[m - 4k][kk]), B = X_k (X's own
+  //    register k), C = X with block row k cleared (its register k)
+  {
+    const double dop = (m >> 2) == K ? Dk[(m & 3) * 4 + kk] : 0.0;
+    d4 Xc = X;
+    Xc[K] = 0.0;
+    X = mfma16x16x4(dop, X[K], Xc);
+  }
   const int cb = col >> 2, j = col & 3;
-  {
-    const double lg0 = sel4(g, l00, l10, l20, l30), lg1 = sel4(g, 0.0, l11, l21, l31),
-                 lg2 = sel4(g, 0.0, 0.0, l22, l32), lg3 = sel4(g, 0.0, 0.0, 0.0, l33);
-    const double lkk = sel4(j, lg0, lg1, lg2, lg3);
-    A[K] = cb == K ? lkk : (cb > K ? 0.0 : A[K]);
-  }
   if constexpr (K < 3) {
-    // 3. L_ik = A_ik D_k^T for the block rows i > k (lanes col = 4k + j): coefficients D[j][m]
-    const double e0 = sel4(j, d00, d10, d20, d30), e1 = sel4(j, 0.0, d11, d21, d31), e2 = sel4(j, 0.0, 0.0, d22, d32),
-                 e3 = sel4(j, 0.0, 0.0, 0.0, d33);
+    // 3. L_ik = A_ik D_k^T for the block rows i > k (lanes col = 4k + j): coefficients D_k[j][0..3]
+    const double2 e01 = *reinterpret_cast<const double2*>(Dk + 4 * j);
+    const double2 e23 = *reinterpret_cast<const double2*>(Dk + 4 * j + 2);
 #pragma unroll
     for (int i = K + 1; i < 4; ++i) {
       const double v0 = quad_bcast_f64<0>(A[i]), v1 = quad_bcast_f64<1>(A[i]), v2 = quad_bcast_f64<2>(A[i]),
                    v3 = quad_bcast_f64<3>(A[i]);
-      const double l = fma(e3, v3, fma(e2, v2, fma(e1, v1, e0 * v0)));
+      const double l = fma(e23.y, v3, fma(e23.x, v2, fma(e01.y, v1, e01.x * v0)));
       A[i] = cb == K ? l : A[i];
     }
-    // 4. operand lane (kk = lane/16, m = lane%16) = L[m][4k+kk] for m > 4k+3: from lane 16 (m%4) + 4k + kk,
-    //    register m/4 (one bpermute per candidate register, then the register select)
-    const int lane = threadIdx.x & 63;
-    const int m = lane & 15, kk = lane >> 4;
+    // 4. operand lane (kk, m) = L[m][4k+kk] for m > 4k+3: from lane 16 (m%4) + 4k + kk, register m/4
     const int src = 16 * (m & 3) + 4 * K + kk;
     double op = 0.0;
 #pragma unroll
@@ -236,9 +301,10 @@ __device__ __forceinline__ void chol16_block_step(d4& A, d4& X, int g, int col, 
   }
 }
 
-// Factor + invert the 16x16 SPD block at (o, o) of sA with one wave, as chol16 (same outputs, same contract).
+// Factor + invert the 16x16 SPD block at (o, o) of sA with one wave, as chol16 (same outputs, same contract); sF: 128
+// doubles of LDS scratch for this wave.
 template <int LDD>
-__device__ __forceinline__ int chol16_mfma(double* sA, double* sD, int o) {
+__device__ __forceinline__ int chol16_mfma(double* sA, double* sD, int o, double* sF) {
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4, col = lane & 15;
   d4 A, X;
@@ -247,18 +313,21 @@ __device__ __forceinline__ int chol16_mfma(double* sA, double* sD, int o) {
     A[q] = sA[(o + g + 4 * q) * LD64 + o + col];
     X[q] = (g + 4 * q == col) ? 1.0 : 0.0;
   }
-  int fail = -1;
-  chol16_block_step<0>(A, X, g, col, fail);
-  chol16_block_step<1>(A, X, g, col, fail);
-  chol16_block_step<2>(A, X, g, col, fail);
-  chol16_block_step<3>(A, X, g, col, fail);
+  unsigned bad = 0;
+  chol16_block_step<0>(A, X, g, col, bad, sF);
+  chol16_block_step<1>(A, X, g, col, bad, sF);
+  chol16_block_step<2>(A, X, g, col, bad, sF);
+  chol16_block_step<3>(A, X, g, col, bad, sF);
+  const int cb = col >> 2, j = col & 3;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int r = g + 4 * q;
-    sA[(o + r) * LD64 + o + col] = col <= r ? A[q] : 0.0;
+    // diagonal 4x4 blocks from the step tables, the rest from the TRSM'd registers
+    const double lv = cb == q ? sF[32 * q + 4 * g + j] : A[q];
+    sA[(o + r) * LD64 + o + col] = col <= r ? lv : 0.0;
     sD[r * LDD + col] = col <= r ? X[q] : 0.0;
   }
-  return fail;
+  return bad ? __builtin_ctz(bad) : -1;
 }
 
 // X = L^{-1} of the lower-triangular 16x16 block at (o, o) of sL (already factored), by one wave: forward

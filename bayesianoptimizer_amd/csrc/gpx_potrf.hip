@@ -36,6 +36,12 @@
 #ifndef GPX_PERSIST_STAMP
 #define GPX_PERSIST_STAMP(kind, c, i, s)
 #endif
+#ifndef GPX_STEP_STAMP
+#define GPX_STEP_STAMP(role, c, b, s)
+#endif
+#ifndef GPX_EAGER_STAMP
+#define GPX_EAGER_STAMP(c, p, i)
+#endif
 
 namespace gpx {
 
@@ -70,8 +76,8 @@ using Tile128 = MfmaTile<2 * NB, 2 * NB, 16, false, false>;  // trailing update
 // Panel: sA, sP (64 x LD64 each) and the two D_ss buffers (16 x LDD); the Tile64 staging of the panel-side
 // update aliases sP + the D buffers (both written only after the update GEMMs).
 constexpr int LDD = 20;
-constexpr int DBUF = 768;  // >= 2 * 16 * LDD, sized so that sP + D buffers hold Tile64::LDS_DOUBLES
-static_assert(NB * LD64 + DBUF >= Tile64::LDS_DOUBLES && DBUF >= 2 * 16 * LDD, "panel LDS aliasing");
+constexpr int DBUF = 768;  // >= 2 * 16 * LDD (+ 128 of chol16_mfma's factor tables), and sP + D buffers hold Tile64::LDS_DOUBLES
+static_assert(NB * LD64 + DBUF >= Tile64::LDS_DOUBLES && DBUF >= 2 * 16 * LDD + 128, "panel LDS aliasing");
 constexpr int PANEL_LDS = 2 * NB * LD64 + DBUF;
 constexpr int STEP_LDS = PANEL_LDS > Tile128::LDS_DOUBLES ? PANEL_LDS : Tile128::LDS_DOUBLES;
 
@@ -92,6 +98,101 @@ __device__ __forceinline__ void update_to_lds(Tile64& tl, const double* __restri
     for (int j = 0; j < Tile64::WN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) S[Tile64::row_of(i, r) * LD64 + Tile64::col_of(j)] = -tl.acc[i][j][r];
+}
+
+// The eager pre-update (K = 64: one pending block column) of a panel workgroup: A_cc -= L_c L_c^T on the 10 lower /
+// diagonal 16-blocks (the strict upper ones are never read by the factorisation) and, for p > 0, A_ic -= L_i L_c^T on
+// all 16, into sA / sP.  Every global load of the step - L_c, L_i and the C seeds of the wave's blocks - is issued in one
+// straight-line burst (MfmaTile's 16-k pipeline exposed a global round trip per k-tile: ~7 us for the two products
+// against ~3 us of MFMA); the seeds are +C and the products subtract through the MFMA's A-operand negation (neg:[1,0,0]),
+// so nothing waits on a seed before the first MFMA needs it.  Wave W owns A_ic's block row W and the A_cc blocks
+// W, W+4, W+8 of the row-major lower list, each a K = 64 chain of 16 MFMAs in MfmaTile's k order (C - ab rounds as
+// -(-C + ab): same results).  sA / sP double as the staging: the products are held in registers across a barrier.
+constexpr int kLowerBlk[10][2] = {{0, 0}, {1, 0}, {1, 1}, {2, 0}, {2, 1}, {2, 2}, {3, 0}, {3, 1}, {3, 2}, {3, 3}};
+
+__device__ __forceinline__ d4 mfma_sub(double a, double b, d4 c) {  // c - a b
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 1);
+}
+
+template <int W, bool PANEL>
+__device__ __forceinline__ void update_eager_wave(const double* __restrict__ Acc, const double* __restrict__ Aic,
+                                                  const double* __restrict__ Lc, const double* __restrict__ Li,
+                                                  int64_t lda, double* sA, double* sP, int c, int p) {
+  constexpr int NCC = W < 2 ? 3 : 2;
+  const int t = threadIdx.x, lane = t & 63;
+  const int g = lane >> 4, cl = lane & 15;
+  double2 rl[8], ri[8];
+  d4 acc_cc[NCC], acc_ic[4];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = (t + q * WG) * 2, r = e >> 6, cc = e & 63;
+    rl[q] = *reinterpret_cast<const double2*>(Lc + (int64_t)r * lda + cc);
+    if (PANEL) ri[q] = *reinterpret_cast<const double2*>(Li + (int64_t)r * lda + cc);
+  }
+#pragma unroll
+  for (int b = 0; b < NCC; ++b) {
+    const int bi = kLowerBlk[W + 4 * b][0], bj = kLowerBlk[W + 4 * b][1];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc_cc[b][q] = Acc[(int64_t)(16 * bi + g + 4 * q) * lda + 16 * bj + cl];
+  }
+  if (PANEL) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc_ic[j][q] = Aic[(int64_t)(16 * W + g + 4 * q) * lda + 16 * j + cl];
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = (t + q * WG) * 2, r = e >> 6, cc = e & 63;
+    *reinterpret_cast<double2*>(sA + r * LD64 + cc) = rl[q];
+    if (PANEL) *reinterpret_cast<double2*>(sP + r * LD64 + cc) = ri[q];
+  }
+  __syncthreads();
+  GPX_EAGER_STAMP(c, p, 0);
+  // k in chunks of 16: one batch of fragment reads (the four L_c row blocks serve as the B operand of every block and as
+  // the A operand of the A_cc blocks; L_i's row block W is A_ic's A operand), then the chunk's MFMAs, independent
+  // across blocks
+  const int m = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int kc = 0; kc < NB; kc += 16) {
+    double fc[4][4], fi[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) fc[jb][s] = sA[(16 * jb + m) * LD64 + kc + 4 * s + kq];
+      if (PANEL) fi[s] = sP[(16 * W + m) * LD64 + kc + 4 * s + kq];
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (PANEL) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc_ic[j] = mfma_sub(fi[s], fc[j][s], acc_ic[j]);
+      }
+#pragma unroll
+      for (int b = 0; b < NCC; ++b)
+        acc_cc[b] = mfma_sub(fc[kLowerBlk[W + 4 * b][0]][s], fc[kLowerBlk[W + 4 * b][1]][s], acc_cc[b]);
+    }
+  }
+  __syncthreads();  // every wave's operand reads done: sA / sP take the results
+  GPX_EAGER_STAMP(c, p, 1);
+#pragma unroll
+  for (int b = 0; b < NCC; ++b) store_block16(sA, 16 * kLowerBlk[W + 4 * b][0], 16 * kLowerBlk[W + 4 * b][1], acc_cc[b]);
+  if (PANEL) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) store_block16(sP, 16 * W, 16 * j, acc_ic[j]);
+  }
+}
+
+template <bool PANEL>
+__device__ __forceinline__ void update_eager(const double* __restrict__ Acc, const double* __restrict__ Aic,
+                                             const double* __restrict__ Lc, const double* __restrict__ Li, int64_t lda,
+                                             double* sA, double* sP, int c, int p) {
+  switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {  // wave-uniform: compile-time block lists per wave
+    case 0: update_eager_wave<0, PANEL>(Acc, Aic, Lc, Li, lda, sA, sP, c, p); break;
+    case 1: update_eager_wave<1, PANEL>(Acc, Aic, Lc, Li, lda, sA, sP, c, p); break;
+    case 2: update_eager_wave<2, PANEL>(Acc, Aic, Lc, Li, lda, sA, sP, c, p); break;
+    default: update_eager_wave<3, PANEL>(Acc, Aic, Lc, Li, lda, sA, sP, c, p); break;
+  }
 }
 
 __device__ __forceinline__ void load_tile_lds(const double* __restrict__ G, int64_t ld, double* S) {
@@ -127,12 +228,22 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
     // factors (K = 64 (c - c0))
     const int kk = (c - c0) * NB;
     const double* Lc = A + (int64_t)c * NB * lda + (int64_t)c0 * NB;
-    Tile64 tl;
-    update_to_lds(tl, Acc, lda, Lc, Lc, lda, kk, smem, sA);
-    if (panel) {
-      __syncthreads();  // smem reuse
-      const double* Li = A + (int64_t)bi * NB * lda + (int64_t)c0 * NB;
-      update_to_lds(tl, Aic, lda, Li, Lc, lda, kk, smem, sP);
+    const double* Li = A + (int64_t)bi * NB * lda + (int64_t)c0 * NB;
+#ifndef GPX_POTRF_TILE_PREUPDATE
+    if (kk == NB) {
+      if (panel)
+        update_eager<true>(Acc, Aic, Lc, Li, lda, sA, sP, c, p);
+      else
+        update_eager<false>(Acc, Aic, Lc, Li, lda, sA, sP, c, p);
+    } else
+#endif
+    {
+      Tile64 tl;
+      update_to_lds(tl, Acc, lda, Lc, Lc, lda, kk, smem, sA);
+      if (panel) {
+        __syncthreads();  // smem reuse
+        update_to_lds(tl, Aic, lda, Li, Lc, lda, kk, smem, sP);
+      }
     }
   } else {
     load_tile_lds(Acc, lda, sA);
@@ -170,7 +281,7 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
       // 4-pivot blocks on v_mfma_f64_16x16x4 (gpx_chol64.h): correct, but measured slower inside the panel (potrf
       // 1.89 vs 1.76 ms at n = 4096): like the rank-1 form it issues ~75 instructions per pivot (selects of the
       // uniform 4x4 factors, cross-row broadcasts) and exposes MFMA / ds_bpermute latency on the chain
-      const int f = chol16_mfma<LDD>(sA, D, o);
+      const int f = chol16_mfma<LDD>(sA, D, o, sDb + 2 * 16 * LDD);
 #endif
       if (f >= 0 && fail < 0) fail = o + f;
     }
@@ -522,12 +633,15 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, int lazy
   const int b = first_wg + (int)blockIdx.x;
   // the panel is the launch's critical path; its waves share SIMDs with trailing tiles' MFMA streams
   if (prio && b < s.npanel) __builtin_amdgcn_s_setprio(3);
-  if (b < s.npanel)
+  const int role = b < s.npanel ? 0 : (b < s.npanel + s.nlook ? 1 : 2);
+  GPX_STEP_STAMP(role, c, b, 0);
+  if (role == 0)
     panel_role(A, lda, c, b, nblk, s.c0, Dinv, info, lds);
-  else if (b < s.npanel + s.nlook)
+  else if (role == 1)
     lookahead_role(A, lda, c, s.look_a, b - s.npanel, lds);
   else
     trailing_role(A, lda, c, nblk, lazy, s.cfirst, b - s.npanel - s.nlook, lds);
+  GPX_STEP_STAMP(role, c, b, 1);
 }
 
 // L_kk from the scratch into A, and D_k = L_kk^{-1} into the first half of Dinv (one workgroup per block).
