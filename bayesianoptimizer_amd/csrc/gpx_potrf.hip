@@ -334,11 +334,11 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
   }
 }
 
-// Trailing workgroup of a flush launch c (c % lazy == 0): 128x128 tile `tile` of the lower triangle of block columns
-// >= cfirst, A_ij -= sum_{k = c-lazy}^{c-1} L_ik L_jk^T (K = 64 lazy).  The 128-grid is aligned to the end of the matrix
+// Trailing workgroup of a flush launch c: 128x128 tile `tile` of the lower triangle of block columns >= cfirst,
+// A_ij -= sum_{k = k0}^{c-1} L_ik L_jk^T (K = 64 (c - k0)).  The 128-grid is aligned to the end of the matrix
 // (first 64-block c0 = nblk - 2M); when it starts at block c, that block row/column is computed but not stored (it
 // belongs to this launch's panel).
-__device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t lda, int c, int nblk, int lazy, int cfirst,
+__device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t lda, int c, int nblk, int k0, int cfirst,
                                               int tile, double* lds) {
   const int m = nblk - cfirst;
   const int M = (m + 1) / 2;
@@ -346,11 +346,11 @@ __device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t ld
   int I, J;
   tri_decode(tile, I, J);
   const int r0 = c0 + 2 * I, q0 = c0 + 2 * J;
-  const double* Li = A + (int64_t)r0 * NB * lda + (int64_t)(c - lazy) * NB;
-  const double* Lj = A + (int64_t)q0 * NB * lda + (int64_t)(c - lazy) * NB;
+  const double* Li = A + (int64_t)r0 * NB * lda + (int64_t)k0 * NB;
+  const double* Lj = A + (int64_t)q0 * NB * lda + (int64_t)k0 * NB;
   double* C = A + (int64_t)r0 * NB * lda + (int64_t)q0 * NB;
   Tile128 tl;
-  tl.run(Li, lda, Lj, lda, 0, lazy * NB, lds);
+  tl.run(Li, lda, Lj, lda, 0, (c - k0) * NB, lds);
   // C - acc, stored for the 64-blocks (rb, cb) with cb >= c+1 and rb >= cb; loads of a row group first (seeding acc with
   // -C before the product, as the 64x64 panel updates do, pushes this 128x128 tile into 30 VGPR spills)
 #pragma unroll
@@ -592,44 +592,44 @@ __global__ void potrf_sync_clear_kernel(int* __restrict__ sync, int words, int64
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < words; e += gridDim.x * blockDim.x) p[e] = 0;
 }
 
-// Work split of launch c.  mode 0: the panels apply the pending columns c0 .. c-1 (c0 = the last flush), the flush
-// (c % lazy == 0) covers columns >= c+1.  mode 1: the panels apply column c-1 only, lookahead workgroups bring
-// column c+1 up to date, the flush covers columns >= c+2.
+// Work split of launch c.  Flush launches (plan.flush) apply the columns k0 .. c-1 (k0 = the previous flush launch, or 0)
+// to the trailing matrix.  mode 0: the panels apply the pending columns c0 = k0 .. c-1, the flush covers columns >= c+1.
+// mode 1: the panels apply column c-1 only, lookahead workgroups bring column c+1 up to date (columns look_a = k0 ..
+// c-1), the flush covers columns >= c+2.  The host decides which launches flush (potrf_flush_interval).
 struct StepPlan {
-  int npanel, nlook, ntrail, c0, look_a, cfirst;
-  bool flush;
+  int npanel, nlook, ntrail, c0, look_a, cfirst, k0, flush;
 };
 
-__host__ __device__ inline StepPlan step_plan(int c, int nblk, int lazy, int mode) {
+inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush) {
   StepPlan s;
   s.npanel = nblk - c;
-  s.flush = c >= lazy && c % lazy == 0;
+  s.flush = flush ? 1 : 0;
+  s.k0 = last_flush;
   if (mode == 0) {
-    s.c0 = c > 0 ? lazy * ((c - 1) / lazy) : 0;
+    s.c0 = c > 0 ? last_flush : 0;
     s.nlook = 0;
     s.look_a = 0;
     s.cfirst = c + 1;
   } else {
     s.c0 = c > 0 ? c - 1 : 0;
     s.nlook = (c >= 1 && c + 1 < nblk) ? nblk - c - 1 : 0;
-    s.look_a = c > 0 ? lazy * ((c - 1) / lazy) : 0;
+    s.look_a = last_flush;
     s.cfirst = c + 2;
   }
   const int m = nblk - s.cfirst;
-  const int M = (s.flush && m > 0) ? (m + 1) / 2 : 0;
+  const int M = (flush && m > 0) ? (m + 1) / 2 : 0;
   s.ntrail = M * (M + 1) / 2;
   return s;
 }
 
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
-potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, int lazy, int mode, double* __restrict__ Dinv,
+potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, StepPlan s, double* __restrict__ Dinv,
                   int32_t* __restrict__ info, int first_wg, int64_t sa, int64_t sd, int prio) {
   A += blockIdx.y * sa;  // problem of a batched fit
   Dinv += blockIdx.y * sd;
   info += blockIdx.y;
   if (*(volatile int32_t*)info != 0) return;  // an earlier step failed: leave the rest untouched
   __shared__ __attribute__((aligned(16))) double lds[STEP_LDS];
-  const StepPlan s = step_plan(c, nblk, lazy, mode);
   const int b = first_wg + (int)blockIdx.x;
   // the panel is the launch's critical path; its waves share SIMDs with trailing tiles' MFMA streams
   if (prio && b < s.npanel) __builtin_amdgcn_s_setprio(3);
@@ -640,7 +640,7 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, int lazy
   else if (role == 1)
     lookahead_role(A, lda, c, s.look_a, b - s.npanel, lds);
   else
-    trailing_role(A, lda, c, nblk, lazy, s.cfirst, b - s.npanel - s.nlook, lds);
+    trailing_role(A, lda, c, nblk, s.k0, s.cfirst, b - s.npanel - s.nlook, lds);
   GPX_STEP_STAMP(role, c, b, 1);
 }
 
@@ -712,19 +712,36 @@ static int potrf_mode(int nblk) {
   return nblk > 64 ? 1 : 0;
 }
 
-int potrf_step_grid(int c, int nblk, int lazy, int mode) {
-  const StepPlan s = step_plan(c, nblk, lazy, mode);
-  return s.npanel + s.nlook + s.ntrail;
+// Flush interval at launch c: `early_g` for the first `early_end` launches (their trailing update is HBM-bound: the
+// C tiles' read + write per flush, not the MFMAs, set the launch length), then potrf_lazy.  GPX_POTRF_EARLY_G /
+// GPX_POTRF_EARLY_END override (0 = one interval throughout).
+static int potrf_flush_interval(int c, int nblk) {
+  static const int eg = env_int("GPX_POTRF_EARLY_G"), ee = env_int("GPX_POTRF_EARLY_END");
+  const int early_g = eg > 0 ? eg : 0, early_end = ee > 0 ? ee : 0;
+  return (early_g > 0 && c < early_end) ? early_g : potrf_lazy(nblk);
+}
+
+// The plan of every launch c < cend (flush launches: c >= 1 and at least one interval after the previous flush).
+template <typename F>
+static void for_each_step(int nblk, int mode, int cend, F&& f) {
+  int last = 0;
+  for (int c = 0; c < cend; ++c) {
+    const bool flush = c >= 1 && c - last >= potrf_flush_interval(c, nblk);
+    f(c, step_plan(c, nblk, mode, last, flush));
+    if (flush) last = c;
+  }
 }
 
 static void launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
                          int cbeg, int cend) {
-  const int lazy = potrf_lazy(nblk), mode = potrf_mode(nblk);
+  const int mode = potrf_mode(nblk);
   static const int prio_env = env_int("GPX_POTRF_PRIO");
   const int prio = prio_env < 0 ? 0 : prio_env;
-  for (int c = cbeg; c < cend; ++c)
-    potrf_step_kernel<<<dim3(potrf_step_grid(c, nblk, lazy, mode), bt.count), WG, 0, ctx->stream>>>(
-        A, lda, c, nblk, lazy, mode, Dinv, info, 0, bt.k, bt.dinv, prio);
+  for_each_step(nblk, mode, cend, [&](int c, const StepPlan& s) {
+    if (c < cbeg) return;
+    const dim3 grid(s.npanel + s.nlook + s.ntrail, bt.count);
+    potrf_step_kernel<<<grid, WG, 0, ctx->stream>>>(A, lda, c, nblk, s, Dinv, info, 0, bt.k, bt.dinv, prio);
+  });
 }
 
 static void launch_dinv(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,

@@ -27,6 +27,8 @@ __device__ unsigned long long g_pan[256][16];
   do {                                                                                                    \
     if (threadIdx.x == 0 && p == (c + 1 < nblk ? 1 : 0) && ((i) == 0 || (i) % 3 == 1 || (i) == 13))       \
       g_pan[c][(i) == 0 ? 1 : ((i) == 13 ? 6 : 2 + (i) / 3)] = wall_clock64();                            \
+    if ((threadIdx.x & 63) == 0 && threadIdx.x > 0 && p == (c + 1 < nblk ? 1 : 0) && (i) % 3 == 0 && (i) > 0 && (i) < 12) \
+      atomicMax(&g_pan[c][9 + (i) / 3 - 1], wall_clock64());                                             \
   } while (0)
 #define GPX_EAGER_STAMP(c, p, i)                                                                          \
   do {                                                                                                    \
@@ -86,6 +88,7 @@ int main(int argc, char** argv) {
   const unsigned long long t0 = f[0];
   auto us = [&](unsigned long long v) { return v ? (double)(long long)(v - t0) / 100.0 : -1.0; };
   double eload = 0, ecomp = 0;
+  double uw[3] = {0, 0, 0};  // waves 1-3 done with step s's U items, relative to wave 0's end of F(s+1)
   double gap = 0, pre = 0, F[4] = {0, 0, 0, 0}, tail = 0, store = 0, wait0 = 0, trail_after = 0;
   int cnt = 0;
   printf("  c   start  panel_end trail_end | crit: start  pre   F0    F1    F2    F3   fact  store\n");
@@ -108,6 +111,7 @@ int main(int argc, char** argv) {
       tail += (double)(P[6] - P[5]) / 100;
       store += (double)(P[15] - P[6]) / 100;
       trail_after += te[c] > pe[c] ? (double)(te[c] - pe[c]) / 100 : 0.0;
+      for (int s = 0; s < 3; ++s) uw[s] += (double)(long long)(P[9 + s] - P[3 + s]) / 100;
       ++cnt;
     }
     (void)end;
@@ -116,6 +120,8 @@ int main(int argc, char** argv) {
          "F steps %.2f %.2f %.2f %.2f, last step tail %.2f, store %.2f, trailing beyond panels %.2f us\n",
          gap / cnt, wait0 / cnt, pre / cnt, F[0] / cnt, F[1] / cnt, F[2] / cnt, F[3] / cnt, tail / cnt, store / cnt,
          trail_after / cnt);
+  printf("waves 1-3 end of U items of step s minus wave 0's end of F(s+1) (> 0: they hold the barrier): s=0 %.2f s=1 %.2f s=2 %.2f us\n",
+         uw[0] / cnt, uw[1] / cnt, uw[2] / cnt);
   printf("eager pre-update split: start -> operands in LDS %.2f us, products %.2f us, stores %.2f us\n", eload / cnt,
          ecomp / cnt, (pre - eload - ecomp) / cnt);
   printf("last launch end %.2f us\n", us(pe[nblk - 1] > te[nblk - 1] ? pe[nblk - 1] : te[nblk - 1]));
