@@ -338,13 +338,47 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
 // A_ij -= sum_{k = k0}^{c-1} L_ik L_jk^T (K = 64 (c - k0)).  The 128-grid is aligned to the end of the matrix
 // (first 64-block c0 = nblk - 2M); when it starts at block c, that block row/column is computed but not stored (it
 // belongs to this launch's panel).
+// Trailing workgroup t of T -> 128-tile (I, J) of the M x M lower grid.  xmap = 0: row-major tile order.  xmap = 1:
+// the tiles in 8 x 8 super-block order, dealt to the XCDs in contiguous chunks (workgroups t, t+8, ... share an XCD:
+// round-robin dispatch, speed only, never correctness), so an XCD's tiles read ~16 L panels through its L2 instead of
+// all of them beside the C stream; the chunking is the bijective XCD swizzle of cdna_hip_programming.md section 5.
+__device__ __forceinline__ void trail_tile(int t, int T, int M, int xmap, int& I, int& J) {
+  if (!xmap) {
+    tri_decode(t, I, J);
+    return;
+  }
+  const int x = t & 7, l = t >> 3, q = T >> 3, r = T & 7;
+  int p = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + l;
+  const int S = (M + 7) >> 3;
+  for (int SI = 0; SI < S; ++SI) {
+    const int rows = M - 8 * SI < 8 ? M - 8 * SI : 8;
+    for (int SJ = 0; SJ <= SI; ++SJ) {
+      const int cnt = SJ < SI ? rows * 8 : rows * (rows + 1) / 2;
+      if (p < cnt) {
+        if (SJ < SI) {
+          I = 8 * SI + (p >> 3);
+          J = 8 * SJ + (p & 7);
+        } else {
+          int i, j;
+          tri_decode(p, i, j);
+          I = 8 * SI + i;
+          J = 8 * SJ + j;
+        }
+        return;
+      }
+      p -= cnt;
+    }
+  }
+  I = J = 0;  // not reached: p < T
+}
+
 __device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t lda, int c, int nblk, int k0, int cfirst,
-                                              int tile, double* lds) {
+                                              int tile, int ntile, int xmap, double* lds) {
   const int m = nblk - cfirst;
   const int M = (m + 1) / 2;
   const int c0 = nblk - 2 * M;
   int I, J;
-  tri_decode(tile, I, J);
+  trail_tile(tile, ntile, M, xmap, I, J);
   const int r0 = c0 + 2 * I, q0 = c0 + 2 * J;
   const double* Li = A + (int64_t)r0 * NB * lda + (int64_t)k0 * NB;
   const double* Lj = A + (int64_t)q0 * NB * lda + (int64_t)k0 * NB;
@@ -598,9 +632,10 @@ __global__ void potrf_sync_clear_kernel(int* __restrict__ sync, int words, int64
 // c-1), the flush covers columns >= c+2.  The host decides which launches flush (potrf_flush_interval).
 struct StepPlan {
   int npanel, nlook, ntrail, c0, look_a, cfirst, k0, flush;
+  int tbase, xmap;  // first trailing workgroup (a multiple of 8 when xmap: XCD-chunked tile order), tile order
 };
 
-inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush) {
+inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush, int xmap = 0) {
   StepPlan s;
   s.npanel = nblk - c;
   s.flush = flush ? 1 : 0;
@@ -619,6 +654,8 @@ inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush)
   const int m = nblk - s.cfirst;
   const int M = (flush && m > 0) ? (m + 1) / 2 : 0;
   s.ntrail = M * (M + 1) / 2;
+  s.xmap = xmap;
+  s.tbase = xmap ? (s.npanel + s.nlook + 7) & ~7 : s.npanel + s.nlook;  // padding workgroups exit at once
   return s;
 }
 
@@ -633,6 +670,7 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, StepPlan
   const int b = first_wg + (int)blockIdx.x;
   // the panel is the launch's critical path; its waves share SIMDs with trailing tiles' MFMA streams
   if (prio && b < s.npanel) __builtin_amdgcn_s_setprio(3);
+  if (b >= s.npanel + s.nlook && b < s.tbase) return;  // alignment padding of the trailing workgroups
   const int role = b < s.npanel ? 0 : (b < s.npanel + s.nlook ? 1 : 2);
   GPX_STEP_STAMP(role, c, b, 0);
   if (role == 0)
@@ -640,7 +678,7 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, StepPlan
   else if (role == 1)
     lookahead_role(A, lda, c, s.look_a, b - s.npanel, lds);
   else
-    trailing_role(A, lda, c, nblk, s.k0, s.cfirst, b - s.npanel - s.nlook, lds);
+    trailing_role(A, lda, c, nblk, s.k0, s.cfirst, b - s.tbase, s.ntrail, s.xmap, lds);
   GPX_STEP_STAMP(role, c, b, 1);
 }
 
@@ -721,13 +759,19 @@ static int potrf_flush_interval(int c, int nblk) {
   return (early_g > 0 && c < early_end) ? early_g : potrf_lazy(nblk);
 }
 
+// Trailing tile order (trail_tile): 1 = XCD-chunked 8 x 8 super-blocks, 0 = row-major.  GPX_POTRF_XMAP overrides.
+static int potrf_xmap() {
+  static const int env = env_int("GPX_POTRF_XMAP");
+  return env >= 0 ? env : 1;
+}
+
 // The plan of every launch c < cend (flush launches: c >= 1 and at least one interval after the previous flush).
 template <typename F>
 static void for_each_step(int nblk, int mode, int cend, F&& f) {
   int last = 0;
   for (int c = 0; c < cend; ++c) {
     const bool flush = c >= 1 && c - last >= potrf_flush_interval(c, nblk);
-    f(c, step_plan(c, nblk, mode, last, flush));
+    f(c, step_plan(c, nblk, mode, last, flush, potrf_xmap()));
     if (flush) last = c;
   }
 }
@@ -739,7 +783,7 @@ static void launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double*
   const int prio = prio_env < 0 ? 0 : prio_env;
   for_each_step(nblk, mode, cend, [&](int c, const StepPlan& s) {
     if (c < cbeg) return;
-    const dim3 grid(s.npanel + s.nlook + s.ntrail, bt.count);
+    const dim3 grid(s.tbase + s.ntrail, bt.count);
     potrf_step_kernel<<<grid, WG, 0, ctx->stream>>>(A, lda, c, nblk, s, Dinv, info, 0, bt.k, bt.dinv, prio);
   });
 }

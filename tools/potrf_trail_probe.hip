@@ -19,6 +19,7 @@ using namespace gpx;
 
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 4096, nblk = n / 64;
+  const int xmap = argc > 2 ? atoi(argv[2]) : 1;  // trailing tile order (trail_tile)
   std::vector<double> h((size_t)n * n), X((size_t)n * 8);
   srand(7);
   for (auto& v : X) v = rand() / (double)RAND_MAX;
@@ -38,19 +39,19 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  auto plan = [&](int c) { return step_plan(c, nblk, 0, c > 0 ? c - 1 : 0, c >= 1); };
+  auto plan = [&](int c) { return step_plan(c, nblk, 0, c > 0 ? c - 1 : 0, c >= 1, xmap); };
   // mode 0 full grid, 1 panel workgroups only, 2 trailing workgroups only
   auto time_step = [&](int c, int mode) {
     CK(hipMemcpy(A, A0, (size_t)n * n * 8, hipMemcpyDeviceToDevice));
     CK(hipMemset(info, 0, 4));
     for (int cc = 0; cc < c; ++cc) {
       const StepPlan s = plan(cc);
-      potrf_step_kernel<<<s.npanel + s.ntrail, WG>>>(A, n, cc, nblk, s, Dinv, info, 0, 0, 0, 0);
+      potrf_step_kernel<<<s.tbase + s.ntrail, WG>>>(A, n, cc, nblk, s, Dinv, info, 0, 0, 0, 0);
     }
     CK(hipDeviceSynchronize());
     const StepPlan s = plan(c);
-    const int grid = mode == 0 ? s.npanel + s.ntrail : mode == 1 ? s.npanel : s.ntrail;
-    const int first = mode == 2 ? s.npanel : 0;
+    const int grid = mode == 0 ? s.tbase + s.ntrail : mode == 1 ? s.npanel : s.ntrail;
+    const int first = mode == 2 ? s.tbase : 0;
     if (grid == 0) return 0.0f;
     CK(hipEventRecord(e0));
     for (int i = 0; i < 20; ++i) potrf_step_kernel<<<grid, WG>>>(A, n, c, nblk, s, Dinv, info, first, 0, 0, 0);
@@ -66,6 +67,6 @@ int main(int argc, char** argv) {
     printf("step %2d: full %6.2f us   panel wgs only %6.2f us (%d)   trailing wgs only %6.2f us (%d tiles)\n", c,
            time_step(c, 0), time_step(c, 1), s.npanel, time_step(c, 2), s.ntrail);
   }
-  printf("TRAIL PROBE DONE\n");
+  printf("xmap=%d TRAIL PROBE DONE\n", xmap);
   return 0;
 }
