@@ -54,7 +54,8 @@ def check_argmax(gpu_idx, scores_ref, scores_gpu, what=""):
 
 # ---- Gram ------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("kind", list(KINDS))
-@pytest.mark.parametrize("n,d", [(1, 1), (77, 3), (129, 8), (300, 32)])
+# n >= ~1400: every 64x64 tile its own workgroup (gridDim.z = 1)
+@pytest.mark.parametrize("n,d", [(1, 1), (77, 3), (129, 8), (300, 32), (1500, 5), (2000, 8)])
 def test_gram(engine, kind, n, d):
     X, _ = O.synthetic_problem(n, d, n + d)
     kp, op = pair(kind, d, outputscale=1.7, noise=3e-4, jitter=1e-6)
