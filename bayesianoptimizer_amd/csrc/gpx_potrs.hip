@@ -4,9 +4,15 @@
 // update of SURVEY §8d (Gram + Cholesky + alpha) no longer forms W = L^{-T} (n^3/3 more flops, 0.61 ms at n = 4096);
 // W is built by gpx_trtri_f64 only when a sweep, a posterior or a gradient needs it.
 //
-// Work items, in order: forward block K = 0 .. nb-1, then backward block K = nb-1 .. 0 (nb = npad / 128).  Item i
-// belongs to workgroup i mod G of its problem (G <= nb workgroups per problem, the grid sized to be co-resident), so
-// an item only ever waits on items with a smaller index, all owned by running workgroups or done.
+// Work items: forward block K = 0 .. nb-1, then backward block K = nb-1 .. 0 (nb = npad / 128).  Workgroup g of a
+// problem (G <= nb workgroups, the grid sized to be co-resident) owns blocks g, g + G, ... in BOTH directions and runs
+// its forward items in ascending block order, then its backward items in descending order.  A forward item waits only
+// on forward items of smaller blocks and a backward item only on backward items of larger blocks (and its own forward
+// result), so the smallest pending forward item and, once every forward item is done, the largest pending backward
+// item can always proceed: no deadlock.  Every workgroup streams nb - 1 tiles in all (block K: K tiles forward,
+// nb - 1 - K backward); the former item-index order (item i on workgroup i mod G) gave workgroup nb-1 both 31-tile items
+// at n = 4096 and made the backward solve wait on its tile stream (`profiles/r02_potrs_timeline.log`: 130 us backward
+// against 90 us forward).
 //   forward K:  v = b_K - sum_{J<K} L_KJ z_J, each 128x128 tile L_KJ loaded into registers BEFORE its z_J is waited
 //               for; then z_K = L_KK^{-1} v with potrf's 64-block inverses: z_a = D_a v_a, v_b -= L_ba z_a,
 //               z_b = D_b v_b.
@@ -324,9 +330,11 @@ __device__ void potrs_items_1(int n, int npad, const double* __restrict__ L, int
   const int t = threadIdx.x, w = t >> 6;
   const int nb = npad / SB;
   const int G = gridDim.x;
-  for (int item = blockIdx.x; item < 2 * nb; item += G) {
-    const bool fwd = item < nb;
-    const int K = fwd ? item : 2 * nb - 1 - item;
+  // blocks g, g + G, ... of this workgroup: forward ascending, then backward descending (see the file comment)
+  const int nown = (nb - (int)blockIdx.x + G - 1) / G;
+  for (int step = 0; step < 2 * nown; ++step) {
+    const bool fwd = step < nown;
+    const int K = (int)blockIdx.x + (fwd ? step : 2 * nown - 1 - step) * G;
     const int64_t r0 = (int64_t)K * SB;
     const int jcount = fwd ? K : nb - 1 - K;
     GPX_POTRS_STAMP(0);
@@ -339,7 +347,8 @@ __device__ void potrs_items_1(int n, int npad, const double* __restrict__ L, int
         load_tile_bwd(R, L, ldl, (int64_t)jblk(jj) * SB, r0);
     };
     if (jcount > 0) load_tile(ta, 0);  // in flight while D_KK is formed
-    form_block_inverse(s, Dinv, L, ldl, K);
+    // the first backward item is the block of the last forward item: its D_KK is still in LDS
+    if (fwd || step != nown) form_block_inverse(s, Dinv, L, ldl, K);
     if (fwd) {
       if (t < SB) s.vs[t] = (r0 + t < n) ? Y[(r0 + t) * ldy] - const_mean : 0.0;
     } else if (w == 0) {
@@ -468,9 +477,11 @@ __device__ void potrs_items(int n, int npad, const double* __restrict__ L, int64
   double* zw = s.zw[w];
   const int nb = npad / SB;
   const int G = gridDim.x;
-  for (int item = blockIdx.x; item < 2 * nb; item += G) {
-    const bool fwd = item < nb;
-    const int K = fwd ? item : 2 * nb - 1 - item;
+  // blocks g, g + G, ... of this workgroup: forward ascending, then backward descending (see the file comment)
+  const int nown = (nb - (int)blockIdx.x + G - 1) / G;
+  for (int step = 0; step < 2 * nown; ++step) {
+    const bool fwd = step < nown;
+    const int K = (int)blockIdx.x + (fwd ? step : 2 * nown - 1 - step) * G;
     const int64_t r0 = (int64_t)K * SB;
     const int jcount = fwd ? K : nb - 1 - K;
     auto jblk = [&](int jj) { return fwd ? jj : nb - 1 - jj; };
@@ -483,9 +494,11 @@ __device__ void potrs_items(int n, int npad, const double* __restrict__ L, int64
     };
     if (jcount > 0) load_tile(ta, 0);
     // diagonal 128-block: D_a, D_b (potrf's inverses of the 64-blocks) and L_ba
-    tile_to_lds(Dinv + (int64_t)(2 * K) * NB * NB, NB, s.Da);
-    tile_to_lds(Dinv + (int64_t)(2 * K + 1) * NB * NB, NB, s.Db);
-    tile_to_lds(L + (r0 + NB) * ldl + r0, ldl, s.Lba);
+    if (fwd || step != nown) {  // the first backward item reuses the last forward item's diagonal block
+      tile_to_lds(Dinv + (int64_t)(2 * K) * NB * NB, NB, s.Da);
+      tile_to_lds(Dinv + (int64_t)(2 * K + 1) * NB * NB, NB, s.Db);
+      tile_to_lds(L + (r0 + NB) * ldl + r0, ldl, s.Lba);
+    }
     if (fwd) {
       for (int e = t; e < SB * NR; e += WG) {
         const int row = e / NR, rr = e % NR;
