@@ -147,9 +147,80 @@ __device__ __forceinline__ void chol16_pivot_fused(Blk16& b, int r, int g, int& 
   fmac_row_bcast8<J>(b.a, b.x, coef, coefx);
 }
 
+// Pipelined pivot J in two asm blocks: (1) the register the next pivot reads, a[QN] (leading/trailing pads: its DPP
+// source may be fresh, and v_readlane / permlane read its result next); (2) the other three a[q] and the four x[q] (their
+// sources were last written a pivot earlier, >= 4 VALU instructions back; block (1) of the next pivot pads again).
+// asm volatile keeps the blocks in order.
+#define GPX_FMAC_PIPE(J)                                                                                         \
+  case J:                                                                                                        \
+    asm volatile("s_nop 1\n\t"                                                                                   \
+                 "v_fmac_f64_dpp %0, %0, %1 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                  \
+                 "s_nop 1"                                                                                       \
+                 : "+v"(an)                                                                                      \
+                 : "v"(ca));                                                                                     \
+    break;
+#define GPX_FMAC_REST(J)                                                                                         \
+  case J:                                                                                                        \
+    asm volatile("v_fmac_f64_dpp %0, %0, %7 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                 \
+                 "v_fmac_f64_dpp %1, %1, %7 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                 \
+                 "v_fmac_f64_dpp %2, %2, %7 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                 \
+                 "v_fmac_f64_dpp %3, %3, %8 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                 \
+                 "v_fmac_f64_dpp %4, %4, %8 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                 \
+                 "v_fmac_f64_dpp %5, %5, %8 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                 \
+                 "v_fmac_f64_dpp %6, %6, %8 row_newbcast:" #J " row_mask:0xf bank_mask:0xf"                       \
+                 : "+v"(a1), "+v"(a2), "+v"(a3), "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3])                  \
+                 : "v"(ca), "v"(cx));                                                                            \
+    break;
+template <int J>
+__device__ __forceinline__ void fmac_pipe_first(double& an, double ca) {
+  switch (J) {
+    GPX_FMAC_PIPE(0) GPX_FMAC_PIPE(1) GPX_FMAC_PIPE(2) GPX_FMAC_PIPE(3) GPX_FMAC_PIPE(4) GPX_FMAC_PIPE(5)
+    GPX_FMAC_PIPE(6) GPX_FMAC_PIPE(7) GPX_FMAC_PIPE(8) GPX_FMAC_PIPE(9) GPX_FMAC_PIPE(10) GPX_FMAC_PIPE(11)
+    GPX_FMAC_PIPE(12) GPX_FMAC_PIPE(13) GPX_FMAC_PIPE(14) GPX_FMAC_PIPE(15)
+  }
+}
+template <int J>
+__device__ __forceinline__ void fmac_pipe_rest(double& a1, double& a2, double& a3, double (&x)[4], double ca, double cx) {
+  switch (J) {
+    GPX_FMAC_REST(0) GPX_FMAC_REST(1) GPX_FMAC_REST(2) GPX_FMAC_REST(3) GPX_FMAC_REST(4) GPX_FMAC_REST(5)
+    GPX_FMAC_REST(6) GPX_FMAC_REST(7) GPX_FMAC_REST(8) GPX_FMAC_REST(9) GPX_FMAC_REST(10) GPX_FMAC_REST(11)
+    GPX_FMAC_REST(12) GPX_FMAC_REST(13) GPX_FMAC_REST(14) GPX_FMAC_REST(15)
+  }
+}
+#undef GPX_FMAC_PIPE
+#undef GPX_FMAC_REST
+
+// chol16_pivot_fused, software-pipelined across pivots: the column register A[.][4g + (J+1)%4] that the NEXT pivot reads
+// (its pivot by v_readlane, its A[r][J+1] by permlane swaps) is updated first, the next pivot's reads are issued, and
+// only then the other seven row-broadcast FMAs of pivot J, so their issue overlaps the readlane -> rsq latency of pivot
+// J+1.  Same operations on the same values as chol16_pivot_fused (bit-identical L and X).
+template <int J>
+__device__ __forceinline__ void chol16_pivot_pipe(Blk16& b, int r, int g, int& fail, double& piv, double& arj) {
+  constexpr int GJ = J >> 2, QJ = J & 3;
+  if (!(piv > 0.0) && fail < 0) fail = J;
+  const double isq = pivot_rsq(piv);
+  const double rinv = isq * isq;
+  const double coef = (r > J) ? -arj * rinv : 0.0;
+  const double coefx = (r == J) ? isq - 1.0 : coef;
+  if (g == GJ) b.l[QJ] = (r >= J) ? b.a[QJ] * isq : 0.0;
+  if constexpr (J < 15) {
+    constexpr int JN = J + 1, GN = JN >> 2, QN = JN & 3;
+    fmac_pipe_first<J>(b.a[QN], coef);
+    piv = readlane_f64(b.a[QN], JN + 16 * GN);
+    arj = xrow_bcast_f64<GN>(b.a[QN]);
+    fmac_pipe_rest<J>(b.a[(QN + 1) & 3], b.a[(QN + 2) & 3], b.a[(QN + 3) & 3], b.x, coef, coefx);
+  } else {
+    fmac_row_bcast8<J>(b.a, b.x, coef, coefx);
+  }
+}
+
 template <int... J>
 __device__ __forceinline__ void chol16_pivots(Blk16& b, int r, int g, int& fail, std::integer_sequence<int, J...>) {
-#ifndef GPX_CHOL16_UNFUSED
+#if !defined(GPX_CHOL16_NOPIPE) && !defined(GPX_CHOL16_UNFUSED)
+  // tools/chol16_probe: 3632 vs 3937 cycles per 16-pivot block unpipelined (potrf n = 4096 1.756 vs 1.767 ms)
+  double piv = readlane_f64(b.a[0], 0), arj = xrow_bcast_f64<0>(b.a[0]);
+  (chol16_pivot_pipe<J>(b, r, g, fail, piv, arj), ...);
+#elif !defined(GPX_CHOL16_UNFUSED)
   (chol16_pivot_fused<J>(b, r, g, fail), ...);
 #else
   (chol16_pivot<J>(b, r, g, fail), ...);
