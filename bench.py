@@ -460,10 +460,28 @@ def main():
     part = {k: eng.timing_query(k) for k in ("gram", "potrf", "alpha")}
     eng.timing_disable()
 
-    times = torch.tensor([elapsed, fit_elapsed], dtype=torch.float64, device=dev)
+    # latency of the cross-GPU exchange alone (report it separately; xGMI bandwidth is irrelevant for a
+    # 16-byte record): back-to-back gpx_allreduce_argmax calls on the step's records, outside the timed step loop
+    xch_us = None
+    if exchange is not None:
+        try:
+            xr = 50
+            barrier(dist)
+            t3 = time.perf_counter()
+            for _ in range(xr):
+                exchange(bv.clone(), bi.clone())
+            torch.cuda.synchronize()
+            xch_us = 1e6 * (time.perf_counter() - t3) / xr
+        except Exception as e:  # a measurement only: never fail the bench line over it
+            print(f"exchange latency not measured: {e}", file=sys.stderr)
+            xch_us = None
+
+    times = torch.tensor([elapsed, fit_elapsed, xch_us if xch_us is not None else -1.0], dtype=torch.float64,
+                         device=dev)
     if dist is not None:
         dist.all_reduce(times, op=dist.ReduceOp.MAX)
     elapsed, fit_elapsed = float(times[0]), float(times[1])
+    xch_us = float(times[2]) if float(times[2]) >= 0 else None
 
     if rank == 0:
         m, n = args.m, args.n
@@ -546,6 +564,9 @@ def main():
                               "frac": gram_gbs / HBM_PEAK_GBS, "bytes_per_launch": gram_bytes,
                               "avg_launch_ms": gram_avg, "launches": part["gram"][1]},
             "cpu_baseline": cpu,
+            "exchange": {"collective": "RCCL all-gather of one 16-byte (value, index) record per rank + combine "
+                                       "kernel (gpx_allreduce_argmax), max over ranks", "latency_us": xch_us}
+            if world > 1 else None,
             "other_configs": extra,
         }
         print(json.dumps(out))
