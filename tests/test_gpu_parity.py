@@ -446,6 +446,26 @@ def test_fit_batched_matches_single_fits_and_oracle(engine, n, B, nrhs, inverse)
         check_posterior(mu.cpu().numpy(), var.cpu().numpy(), mu_r, var_r, O.kernel_diag(Xq, op))
 
 
+def test_fit_batched_potrs_multiblock_owners(engine):
+    """Batched factor-only fits where the solve's workgroups own several 128-row blocks each (gpx_potrs: G = 256 / B = 64
+    workgroups per problem < nb = 65 blocks at n = 8320, B = 4; forward ascending then backward descending per
+    workgroup): alpha bit-identical to single fits (G = 65, one block each), and against the oracle's alpha."""
+    n, d, B = 8320, 8, 4
+    kp, op = pair("rbf", d, noise=1e-3)
+    Xs, ys = [], []
+    for b in range(B):
+        X, y = O.synthetic_problem(n, d, 300 + b)
+        Xs.append(X)
+        ys.append(y)
+    sts = engine.fit_batched(t(np.stack(Xs)), t(np.stack(ys)), kp)
+    for b in (0, B - 1):
+        single = engine.fit(t(Xs[b]), t(ys[b]), kp)
+        assert torch.equal(sts[b].alpha, single.alpha)
+    a = sts[B - 1].alpha[:n].cpu().numpy().reshape(-1)
+    a_r = O.fit(Xs[B - 1], ys[B - 1], op).alpha.reshape(-1)
+    assert np.abs(a - a_r).max() <= 1e-6 * np.abs(a_r).max()
+
+
 def test_configs3_per_gpu_share_batched_n4096(engine):
     """BASELINE configs[3] (32 independent restarts x n=4096 d=8 over 8 GPUs) at its per-GPU share: 4 problems fitted in
     the same launches (gpx_fit_batched_f64), each bit-identical to its own single fit, each with a 2^20-candidate logEI
