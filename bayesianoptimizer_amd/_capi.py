@@ -19,6 +19,8 @@ GPX_MAX_DIM = 32
 GPX_MAX_RHS = 8
 GPX_TILE = 128
 GPX_MAX_Q = 32
+GPX_ALLOC_DEFAULT = 0
+GPX_ALLOC_UNCACHED = 1
 GPX_MAX_GRAD_CANDIDATES = 16384
 GPX_COMM_ID_BYTES = 128
 
@@ -90,6 +92,8 @@ _PROTOS = {
     "gpx_padded_n": (c_int64, [c_int64]),
     "gpx_kernel_params_size": (c_size_t, []),
     "gpx_acq_params_size": (c_size_t, []),
+    "gpx_device_alloc": (c_int32, [_h, c_size_t, c_int32, POINTER(c_void_p)]),
+    "gpx_device_free": (c_int32, [_h, c_void_p]),
     "gpx_gram_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64]),
     "gpx_potrf_f64": (c_int32, [_h, c_int64, _p, c_int64, _p, _p]),
     "gpx_trtri_workspace_size": (c_int32, [c_int64, POINTER(c_size_t)]),

@@ -162,6 +162,28 @@ gpx_status gpx_set_stream(gpx_handle h, void* stream) {
   return GPX_OK;
 }
 
+gpx_status gpx_device_alloc(gpx_handle h, size_t bytes, int32_t flags, void** out) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_NONNULL(c, out);
+  *out = nullptr;
+  if (flags != GPX_ALLOC_DEFAULT && flags != GPX_ALLOC_UNCACHED) return fail(c, GPX_INVALID_ARG, "flags");
+  if (bytes == 0) return GPX_OK;
+  GPX_USE_DEVICE(c);
+  const hipError_t e = flags == GPX_ALLOC_UNCACHED ? hipExtMallocWithFlags(out, bytes, hipDeviceMallocUncached)
+                                                   : hipMalloc(out, bytes);
+  if (e != hipSuccess) *out = nullptr;
+  return hip_check(c, e, "device alloc");
+}
+
+gpx_status gpx_device_free(gpx_handle h, void* ptr) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  if (!ptr) return GPX_OK;
+  GPX_USE_DEVICE(c);
+  return hip_check(c, hipFree(ptr), "device free");
+}
+
 const char* gpx_last_error(gpx_handle h) {
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return "invalid handle";

@@ -38,6 +38,31 @@ def botorch_default_lengthscale(d: int) -> float:
     return math.exp(math.sqrt(2.0) + 0.5 * math.log(d) - 3.0)
 
 
+class _FactorBuffer:
+    """fp64 device memory from gpx_device_alloc (include/gpx.h), exposed to torch through __cuda_array_interface__:
+    ``torch.as_tensor`` keeps this object alive for as long as any view of the memory lives, and the object keeps its
+    engine (so the handle outlives the allocation).  GPX_ALLOC_UNCACHED keeps the factored matrix's lines out of the
+    XCD L2s' dirty set, which shortens every kernel boundary of the multi-launch Cholesky."""
+
+    def __init__(self, engine: "GPEngine", shape, flags: int):
+        self.engine = engine
+        self.ptr = None
+        nbytes = 8 * math.prod(shape)
+        p = ctypes.c_void_p()
+        _capi.check(engine.lib.gpx_device_alloc(engine.handle, nbytes, flags, ctypes.byref(p)), engine.handle)
+        self.ptr = p.value
+        self.__cuda_array_interface__ = {"shape": tuple(int(v) for v in shape), "typestr": "<f8",
+                                         "data": (self.ptr, False), "strides": None, "version": 2}
+
+    def __del__(self):
+        try:
+            if self.ptr and self.engine.handle is not None:
+                self.engine.lib.gpx_device_free(self.engine.handle, ctypes.c_void_p(self.ptr))
+        except Exception:
+            pass
+        self.ptr = None
+
+
 @dataclass
 class KernelParams:
     """Fixed GP hyperparameters (the arguments of the reference's covar_module/likelihood/mean)."""
@@ -192,13 +217,26 @@ class GPEngine:
         return ((n + _capi.GPX_TILE - 1) // _capi.GPX_TILE) * _capi.GPX_TILE
 
     # -- fit --------------------------------------------------------------------------------------
+    def factor_buffer(self, shape) -> torch.Tensor:
+        """A zero-copy fp64 device tensor for a matrix the Cholesky factors in place: uncached (GPX_ALLOC_UNCACHED) unless
+        GPX_UNCACHED_FACTOR=0 (A/B measurements), else an ordinary torch allocation."""
+        if not hasattr(self, "_uncached_factor"):
+            import os
+            self._uncached_factor = os.environ.get("GPX_UNCACHED_FACTOR", "1") != "0"
+        if not self._uncached_factor or math.prod(shape) == 0:
+            return torch.empty(tuple(shape), dtype=torch.float64, device=self.device)
+        t = torch.as_tensor(_FactorBuffer(self, shape, _capi.GPX_ALLOC_UNCACHED), device=self.device)
+        if t.dtype != torch.float64 or tuple(t.shape) != tuple(shape) or not t.is_cuda:
+            raise GPXError(_capi.GPX_HIP_ERROR, "factor buffer: unexpected tensor from __cuda_array_interface__")
+        return t
+
     def alloc_state(self, X: torch.Tensor, nrhs: int, params: KernelParams, capacity: int = 0) -> GPState:
         """Device buffers of one GP; ``capacity`` (training points) reserves room for later ``append`` calls."""
         n = X.shape[0]
         npad = self.padded_n(n)
         cap = max(npad, self.padded_n(capacity)) if capacity else npad
         dev = self.device
-        Lbuf = torch.empty((cap, cap), dtype=torch.float64, device=dev)
+        Lbuf = self.factor_buffer((cap, cap))
         Wbuf = torch.empty((cap, cap), dtype=torch.float64, device=dev)
         return GPState(
             X=X,
@@ -392,7 +430,7 @@ class GPEngine:
             Lb, Wb, Db, Ab, Ib = out[0]._batch
         else:
             dev = self.device
-            Lb = torch.empty((B, npad, npad), dtype=torch.float64, device=dev)
+            Lb = self.factor_buffer((B, npad, npad))
             Wb = torch.empty((B, npad, npad), dtype=torch.float64, device=dev)
             Db = torch.empty((B, 2 * nblk, 64, 64), dtype=torch.float64, device=dev)
             Ab = torch.empty((B, npad, nrhs), dtype=torch.float64, device=dev)

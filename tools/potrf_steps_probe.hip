@@ -54,7 +54,13 @@ int main(int argc, char** argv) {
     }
   double *A, *Dv;
   int32_t* info;
-  CK(hipMalloc(&A, hA.size() * 8));
+  // argv[2]: allocation of the factored matrix (0 hipMalloc, 1 fine-grained, 3 uncached): whether the kernel-boundary
+  // L2 write-back of dirty lines is what the launch gap pays
+  const int amode = argc > 2 ? atoi(argv[2]) : 0;
+  if (amode == 0)
+    CK(hipMalloc(&A, hA.size() * 8));
+  else
+    CK(hipExtMallocWithFlags((void**)&A, hA.size() * 8, amode));
   CK(hipMalloc(&Dv, (size_t)2 * nblk * 4096 * 8));
   CK(hipMalloc(&info, 4));
   Context ctx;
@@ -84,7 +90,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpyFromSymbol(pe.data(), HIP_SYMBOL(g_pend), 2048));
   CK(hipMemcpyFromSymbol(te.data(), HIP_SYMBOL(g_tend), 2048));
   CK(hipMemcpyFromSymbol(pan.data(), HIP_SYMBOL(g_pan), 256 * 16 * 8));
-  printf("n=%d nblk=%d: potrf %.3f ms (hipEvent, incl. dinv), info=%d\n", n, nblk, ms, hinfo);
+  printf("n=%d nblk=%d alloc=%d: potrf %.3f ms (hipEvent, incl. dinv), info=%d\n", n, nblk, amode, ms, hinfo);
   const unsigned long long t0 = f[0];
   auto us = [&](unsigned long long v) { return v ? (double)(long long)(v - t0) / 100.0 : -1.0; };
   double eload = 0, ecomp = 0;
