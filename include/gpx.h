@@ -128,8 +128,9 @@ size_t gpx_acq_params_size(void);
 /* Device memory for the factored matrix (no reference counterpart: an allocation policy of this library).  flags:
  * GPX_ALLOC_DEFAULT (hipMalloc) or GPX_ALLOC_UNCACHED (hipExtMallocWithFlags(hipDeviceMallocUncached): lines of the
  * buffer are not kept dirty in the XCD L2s, so the kernel-boundary write-back between the Cholesky's dependent launches
- * has nothing to flush: launch gap 3.3 -> 1.8 us, potrf n = 4096 1.75 -> 1.67 ms).  Freed with
- * gpx_device_free on the same handle's device. */
+ * has nothing to flush: launch gap 3.3 -> 1.8 us, potrf n = 4096 1.75 -> 1.67 ms).  EXPERIMENTAL: a batched fit
+ * on an uncached factor differed from its single fit in the last bits on one box, so the Python engine does not use
+ * it by default.  Freed with gpx_device_free on the same handle's device. */
 #define GPX_ALLOC_DEFAULT 0
 #define GPX_ALLOC_UNCACHED 1
 gpx_status gpx_device_alloc(gpx_handle h, size_t bytes, int32_t flags, void** out);
