@@ -19,13 +19,15 @@ GPX_MAX_DIM = 32
 GPX_MAX_RHS = 8
 GPX_TILE = 128
 GPX_MAX_Q = 32
-GPX_ALLOC_DEFAULT = 0
-GPX_ALLOC_UNCACHED = 1
 GPX_MAX_GRAD_CANDIDATES = 16384
 GPX_COMM_ID_BYTES = 128
 
-GPX_OK, GPX_NOT_PD, GPX_INVALID_ARG, GPX_HIP_ERROR, GPX_RCCL_ERROR = 0, 1, 2, 3, 4
-STATUS_NAMES = {0: "OK", 1: "NOT_PD", 2: "INVALID_ARG", 3: "HIP_ERROR", 4: "RCCL_ERROR"}
+GPX_OK, GPX_NOT_PD, GPX_INVALID_ARG, GPX_HIP_ERROR, GPX_RCCL_ERROR, GPX_TIMEOUT = 0, 1, 2, 3, 4, 5
+STATUS_NAMES = {0: "OK", 1: "NOT_PD", 2: "INVALID_ARG", 3: "HIP_ERROR", 4: "RCCL_ERROR", 5: "TIMEOUT"}
+GPX_INFO_TIMEOUT = -(2 ** 31)  # device info word of a factorisation / solve whose in-launch hand-off timed out
+
+# per-handle options (include/gpx.h GPX_OPT_*)
+OPTIONS = {"potrf_schedule": 0, "spin_limit": 1, "sweep_fused": 2, "gram_split": 3, "potrf_lazy": 4, "potrf_mode": 5}
 
 KERNEL_RBF, KERNEL_MATERN52, KERNEL_SCALE_LINEAR_MATERN52 = 0, 1, 2
 ACQ_EI, ACQ_LOGEI, ACQ_UCB, ACQ_VARIANCE = 0, 1, 2, 3
@@ -53,6 +55,27 @@ class NotPositiveDefiniteError(GPXError):
     def __init__(self, pivot: int, message: str = ""):
         super().__init__(GPX_NOT_PD, message or f"matrix not positive definite at pivot {pivot}")
         self.pivot = pivot
+
+
+class GPXTimeoutError(GPXError):
+    """A persistent launch (the dataflow Cholesky or the triangular solve) gave up on an in-launch hand-off after its
+    bounded spin: the factor / alpha of that call are invalid.  Distinct from NotPositiveDefiniteError, because a larger
+    jitter (the reference's retry, optimization/Bayesian6.py:481-488) does not cure it."""
+
+    def __init__(self, message: str = ""):
+        super().__init__(GPX_TIMEOUT, message or "in-launch hand-off timed out (GPX_OPT_SPIN_LIMIT)")
+
+
+def info_error(value: int, what: str = ""):
+    """The exception a device ``info`` word stands for (None for 0): NotPositiveDefiniteError for a failed pivot
+    (value = pivot + 1 > 0), GPXTimeoutError for GPX_INFO_TIMEOUT (any negative value)."""
+    value = int(value)
+    prefix = f"{what}: " if what else ""
+    if value > 0:
+        return NotPositiveDefiniteError(value - 1, f"{prefix}not positive definite at pivot {value - 1}")
+    if value < 0:
+        return GPXTimeoutError(f"{prefix}in-launch hand-off timed out (info {value})")
+    return None
 
 
 class KernelParamsC(ctypes.Structure):
@@ -92,8 +115,8 @@ _PROTOS = {
     "gpx_padded_n": (c_int64, [c_int64]),
     "gpx_kernel_params_size": (c_size_t, []),
     "gpx_acq_params_size": (c_size_t, []),
-    "gpx_device_alloc": (c_int32, [_h, c_size_t, c_int32, POINTER(c_void_p)]),
-    "gpx_device_free": (c_int32, [_h, c_void_p]),
+    "gpx_set_option": (c_int32, [_h, c_int32, c_int64]),
+    "gpx_get_option": (c_int32, [_h, c_int32, POINTER(c_int64)]),
     "gpx_gram_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64]),
     "gpx_potrf_f64": (c_int32, [_h, c_int64, _p, c_int64, _p, _p]),
     "gpx_trtri_workspace_size": (c_int32, [c_int64, POINTER(c_size_t)]),
@@ -200,4 +223,6 @@ def check(status: int, handle=None):
     if handle is not None and _lib is not None:
         raw = _lib.gpx_last_error(handle)
         msg = raw.decode() if raw else ""
+    if status == GPX_TIMEOUT:
+        raise GPXTimeoutError(msg)
     raise GPXError(status, msg)

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -122,6 +123,8 @@ size_t gpx_kernel_params_size(void) { return sizeof(gpx_kernel_params); }
 
 size_t gpx_acq_params_size(void) { return sizeof(gpx_acq_params); }
 
+static void apply_env_options(Context* c);
+
 gpx_status gpx_create(int32_t device, gpx_handle* out) {
   if (!out) return GPX_INVALID_ARG;
   *out = nullptr;
@@ -131,6 +134,7 @@ gpx_status gpx_create(int32_t device, gpx_handle* out) {
   Context* c = new (std::nothrow) Context();
   if (!c) return GPX_HIP_ERROR;
   c->device = device;
+  apply_env_options(c);
   {
     gpx::DeviceScope dev(device);  // the device must be selectable; the caller's current device is left as it was
     if (dev.err != hipSuccess) {
@@ -151,6 +155,10 @@ gpx_status gpx_destroy(gpx_handle h) {
     (void)hipEventDestroy(pt.stop);
   }
   for (auto ev : c->free_events) (void)hipEventDestroy(ev);
+  {
+    gpx::DeviceScope dev(c->device);
+    gpx::potrf_dag_release(c);
+  }
   delete c;
   return GPX_OK;
 }
@@ -162,26 +170,84 @@ gpx_status gpx_set_stream(gpx_handle h, void* stream) {
   return GPX_OK;
 }
 
-gpx_status gpx_device_alloc(gpx_handle h, size_t bytes, int32_t flags, void** out) {
-  Context* c = reinterpret_cast<Context*>(h);
-  if (!c) return GPX_INVALID_ARG;
-  GPX_NONNULL(c, out);
-  *out = nullptr;
-  if (flags != GPX_ALLOC_DEFAULT && flags != GPX_ALLOC_UNCACHED) return fail(c, GPX_INVALID_ARG, "flags");
-  if (bytes == 0) return GPX_OK;
-  GPX_USE_DEVICE(c);
-  const hipError_t e = flags == GPX_ALLOC_UNCACHED ? hipExtMallocWithFlags(out, bytes, hipDeviceMallocUncached)
-                                                   : hipMalloc(out, bytes);
-  if (e != hipSuccess) *out = nullptr;
-  return hip_check(c, e, "device alloc");
+static gpx_status set_option(Context* c, int32_t option, int64_t v) {
+  switch (option) {
+    case GPX_OPT_POTRF_SCHEDULE:
+      if (v < 0 || v > 2) return fail(c, GPX_INVALID_ARG, "potrf_schedule must be 0, 1 or 2");
+      c->potrf_schedule = (int)v;
+      return GPX_OK;
+    case GPX_OPT_SPIN_LIMIT:
+      if (v < 0 || v > 0x7fffffff) return fail(c, GPX_INVALID_ARG, "spin_limit must be in [0, 2^31)");
+      c->spin_limit = (unsigned)v;
+      return GPX_OK;
+    case GPX_OPT_SWEEP_FUSED:
+      if (v != 0 && v != 1) return fail(c, GPX_INVALID_ARG, "sweep_fused must be 0 or 1");
+      c->sweep_fused = (int)v;
+      return GPX_OK;
+    case GPX_OPT_GRAM_SPLIT:
+      if (v != 0 && v != 1 && v != 2 && v != 4) return fail(c, GPX_INVALID_ARG, "gram_split must be 0, 1, 2 or 4");
+      c->gram_split = (int)v;
+      return GPX_OK;
+    case GPX_OPT_POTRF_LAZY:
+      if (v < 0 || v > 16) return fail(c, GPX_INVALID_ARG, "potrf_lazy must be in [0, 16]");
+      c->potrf_lazy = (int)v;
+      return GPX_OK;
+    case GPX_OPT_POTRF_MODE:
+      if (v < -1 || v > 1) return fail(c, GPX_INVALID_ARG, "potrf_mode must be -1, 0 or 1");
+      c->potrf_mode = (int)v;
+      return GPX_OK;
+    default:
+      return fail(c, GPX_INVALID_ARG, "unknown option " + std::to_string(option));
+  }
 }
 
-gpx_status gpx_device_free(gpx_handle h, void* ptr) {
+static int option_by_name(const std::string& name) {
+  static const char* names[GPX_OPT_COUNT] = {"potrf_schedule", "spin_limit", "sweep_fused",
+                                             "gram_split",     "potrf_lazy", "potrf_mode"};
+  for (int i = 0; i < GPX_OPT_COUNT; ++i)
+    if (name == names[i]) return i;
+  return -1;
+}
+
+// GPX_OPTIONS="name=value,...": the library's only read of the environment (tuning / A-B tools)
+static void apply_env_options(Context* c) {
+  const char* e = std::getenv("GPX_OPTIONS");
+  if (!e) return;
+  std::string all(e);
+  size_t pos = 0;
+  while (pos < all.size()) {
+    size_t end = all.find(',', pos);
+    if (end == std::string::npos) end = all.size();
+    const std::string item = all.substr(pos, end - pos);
+    const size_t eq = item.find('=');
+    if (eq != std::string::npos) {
+      const int opt = option_by_name(item.substr(0, eq));
+      if (opt >= 0) (void)set_option(c, opt, std::atoll(item.c_str() + eq + 1));
+    }
+    pos = end + 1;
+  }
+  c->last_error.clear();
+}
+
+gpx_status gpx_set_option(gpx_handle h, int32_t option, int64_t value) {
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return GPX_INVALID_ARG;
-  if (!ptr) return GPX_OK;
-  GPX_USE_DEVICE(c);
-  return hip_check(c, hipFree(ptr), "device free");
+  return set_option(c, option, value);
+}
+
+gpx_status gpx_get_option(gpx_handle h, int32_t option, int64_t* value_host) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_NONNULL(c, value_host);
+  switch (option) {
+    case GPX_OPT_POTRF_SCHEDULE: *value_host = c->potrf_schedule; return GPX_OK;
+    case GPX_OPT_SPIN_LIMIT: *value_host = c->spin_limit; return GPX_OK;
+    case GPX_OPT_SWEEP_FUSED: *value_host = c->sweep_fused; return GPX_OK;
+    case GPX_OPT_GRAM_SPLIT: *value_host = c->gram_split; return GPX_OK;
+    case GPX_OPT_POTRF_LAZY: *value_host = c->potrf_lazy; return GPX_OK;
+    case GPX_OPT_POTRF_MODE: *value_host = c->potrf_mode; return GPX_OK;
+    default: return fail(c, GPX_INVALID_ARG, "unknown option " + std::to_string(option));
+  }
 }
 
 const char* gpx_last_error(gpx_handle h) {
@@ -363,6 +429,8 @@ gpx_status gpx_fit_f64_sync(gpx_handle h, const gpx_kernel_params* p, int64_t n,
   GPX_TRY(hip_check(c, hipMemcpyAsync(&hinfo, info, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream), "info D2H"));
   GPX_TRY(hip_check(c, hipStreamSynchronize(c->stream), "sync"));
   if (info_host) *info_host = hinfo;
+  if (hinfo == GPX_INFO_TIMEOUT)
+    return fail(c, GPX_TIMEOUT, "an in-launch hand-off of the factorisation timed out (spin limit)");
   if (hinfo != 0)
     return fail(c, GPX_NOT_PD, "Gram matrix not positive definite at pivot " + std::to_string(hinfo - 1));
   return GPX_OK;
@@ -376,17 +444,17 @@ gpx_status gpx_potrs_workspace_size(int64_t n, int64_t nrhs, size_t* bytes) {
 
 static gpx_status potrs_impl(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv,
                              const double* Y, int64_t ldy, int64_t nrhs, double const_mean, double* alpha,
-                             const int32_t* info, void* ws, size_t ws_bytes, bool ws_cleared);
+                             int32_t* info, void* ws, size_t ws_bytes, bool ws_cleared);
 
 gpx_status gpx_potrs_f64(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv, const double* Y,
-                         int64_t ldy, int64_t nrhs, double const_mean, double* alpha, const int32_t* info, void* ws,
+                         int64_t ldy, int64_t nrhs, double const_mean, double* alpha, int32_t* info, void* ws,
                          size_t ws_bytes) {
   return potrs_impl(h, n, L, ldl, Dinv, Y, ldy, nrhs, const_mean, alpha, info, ws, ws_bytes, false);
 }
 
 static gpx_status potrs_impl(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv,
                              const double* Y, int64_t ldy, int64_t nrhs, double const_mean, double* alpha,
-                             const int32_t* info, void* ws, size_t ws_bytes, bool ws_cleared) {
+                             int32_t* info, void* ws, size_t ws_bytes, bool ws_cleared) {
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return GPX_INVALID_ARG;
   GPX_TRY(check_n(c, n));

@@ -30,6 +30,19 @@ struct Context {
   int64_t timer_launches[GPX_TIMER_COUNT] = {0};
   std::vector<PendingTimer> pending;
   std::vector<hipEvent_t> free_events;
+  // persistent dataflow Cholesky (gpx_potrf_dag.hip): CU count, task-list cache, zeroed-per-call sync words
+  int cu_count = 0;
+  void* dag_cache = nullptr;
+  void* dag_sync = nullptr;
+  size_t dag_sync_bytes = 0;
+  // bounded spins of the in-launch hand-offs (potrf DAG, potrs): passes before a waiter gives up and reports a timeout
+  unsigned spin_limit = 1u << 22;
+  // options (include/gpx.h GPX_OPT_*; set by gpx_set_option or GPX_OPTIONS at gpx_create)
+  int potrf_schedule = 0;  // 0 by size (dataflow for npad <= 4096), 1 multi-launch, 2 dataflow where it applies
+  int sweep_fused = 1;     // fused small-n sweep where it applies
+  int gram_split = 0;      // 0 by size, else workgroups per Gram tile
+  int potrf_lazy = 0;      // multi-launch flush interval, 0 by size
+  int potrf_mode = -1;     // multi-launch panel mode, -1 by size
 };
 
 // Scoped device switch of one C ABI call: makes the handle's device current and restores the caller's current device
@@ -81,6 +94,12 @@ hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, 
 // with launch_trtri(..., diag_done = true) saves one dispatch.
 hipError_t launch_potrf(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info,
                         const Batch& bt = Batch(), double* W = nullptr, int64_t ldw = 0);
+// the persistent dataflow schedule for npad <= 4096 (gpx_potrf_dag.hip); launch_potrf uses it when
+// potrf_dag_workers() > 0
+int potrf_dag_workers(Context* c, int npad, int batch);
+hipError_t launch_potrf_dag(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info,
+                            const Batch& bt, double* W, int64_t ldw);
+void potrf_dag_release(Context* c);
 hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, const double* Dinv, double* W,
                         int64_t ldw, double* T, const Batch& bt = Batch(), bool diag_done = false);
 hipError_t launch_alpha(Context* c, int n, int npad, const double* W, int64_t ldw, const double* Y, int64_t ldy,
@@ -93,7 +112,7 @@ size_t potrs_workspace_bytes(int64_t npad, int64_t nrhs, int64_t batch);
 size_t potrs_clear_bytes(int64_t npad, int64_t nrhs, int64_t batch);
 hipError_t launch_potrs(Context* c, int n, int npad, const double* L, int64_t ldl, const double* Dinv,
                         const double* Y, int64_t ldy, int nrhs, double const_mean, double* alpha,
-                        const int32_t* info, void* ws, const Batch& bt = Batch(), bool ws_cleared = false);
+                        int32_t* info, void* ws, const Batch& bt = Batch(), bool ws_cleared = false);
 
 struct SweepBuffers {
   double* kstar;     // npad x C

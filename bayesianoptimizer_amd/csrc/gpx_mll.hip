@@ -255,13 +255,9 @@ __global__ void __launch_bounds__(WG) mll_finalize_kernel(int n, int nrhs, const
 // k-chunk of the split.  n = 4096 (tools/mll_probe.hip): kc 512 / 1024 / 2048 / npad -> 0.670 / 0.620 / 0.678 /
 // 0.742 ms: a shallower chunk balances the deep tiles, but the dK epilogue runs once per unit; n = 8192
 // (tools/mll_kc_sweep.sh): 512 / 1024 / 2048 -> 5.33 / 4.74 / 4.65 ms; n = 16384: 2048 / 4096 / 8192 / 16384 ->
-// 28.0 / 27.1 / 26.2 / 26.1 ms (thousands of tiles balance themselves).  GPX_MLL_KC overrides.
+// 28.0 / 27.1 / 26.2 / 26.1 ms (thousands of tiles balance themselves).
 int mll_kchunk(int64_t npad) {
-  static const int env = [] {
-    const char* e = std::getenv("GPX_MLL_KC");
-    return e ? std::atoi(e) : 0;
-  }();
-  int64_t kc = env > 0 ? env : (npad >= 16384 ? npad / 2 : npad / 4);
+  int64_t kc = npad >= 16384 ? npad / 2 : npad / 4;
   kc = ((kc + MT - 1) / MT) * MT;
   return (int)(kc < 512 ? 512 : kc);
 }

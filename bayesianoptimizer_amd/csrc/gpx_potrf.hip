@@ -27,14 +27,10 @@
 #include "gpx_internal.h"
 #include "gpx_device.h"
 #include "gpx_chol64.h"
-#include <cstdlib>
 
 // Optional timestamp hook for tools/potrf_bench.hip (compiled out in the library).
 #ifndef GPX_PANEL_STAMP
 #define GPX_PANEL_STAMP(i)
-#endif
-#ifndef GPX_PERSIST_STAMP
-#define GPX_PERSIST_STAMP(kind, c, i, s)
 #endif
 #ifndef GPX_STEP_STAMP
 #define GPX_STEP_STAMP(role, c, b, s)
@@ -44,30 +40,6 @@
 #endif
 
 namespace gpx {
-
-// Write-through (sc1) stores through a raw buffer resource: one SGPR descriptor + a 32-bit lane offset per store (the
-// 64-bit-address atomic-store form of the same store pushed the persistent trailing role into scratch spills).
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-constexpr int kAuxSC1 = 16;  // cache-policy operand of the buffer intrinsics: sc1 (write-through, agent coherent)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(void* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
-}
-#ifndef GPX_PROBE_PLAIN_STORES  // timing experiments only (tools/potrf_probe.hip); never defined in the library
-constexpr int kStoreAux = kAuxSC1;
-#else
-constexpr int kStoreAux = 0;
-#endif
-__device__ __forceinline__ void store_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, double v) {
-  const unsigned long long b = __double_as_longlong(v);
-  const u32x2 x = {(unsigned)b, (unsigned)(b >> 32)};
-  __builtin_amdgcn_raw_buffer_store_b64(x, r, byte_off, 0, kStoreAux);
-}
-__device__ __forceinline__ void store_sc1(__amdgpu_buffer_rsrc_t r, int byte_off, double v0, double v1) {
-  const unsigned long long b0 = __double_as_longlong(v0), b1 = __double_as_longlong(v1);
-  const u32x4 x = {(unsigned)b0, (unsigned)(b0 >> 32), (unsigned)b1, (unsigned)(b1 >> 32)};
-  __builtin_amdgcn_raw_buffer_store_b128(x, r, byte_off, 0, kStoreAux);
-}
 
 using Tile64 = MfmaTile<NB, NB, 16, false, false>;        // panel-side update (one 64x64 tile)
 using Tile128 = MfmaTile<2 * NB, 2 * NB, 16, false, false>;  // trailing update
@@ -206,9 +178,7 @@ __device__ __forceinline__ void load_tile_lds(const double* __restrict__ G, int6
   }
 }
 
-// Panel workgroup p of block column c (see the file comment).  SC1: the L_ic tile is stored write-through (agent-scope
-// atomic 8-byte stores) for the in-launch hand-off of the persistent schedule.
-template <bool SC1 = false>
+// Panel workgroup p of block column c (see the file comment).
 __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, int c, int p, int nblk, int c0,
                                            double* __restrict__ Dinv, int32_t* __restrict__ info, double* lds) {
   double* sA = lds;             // A_cc -> L_cc
@@ -326,11 +296,7 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int e = (t + q * WG) * 2, r = e >> 6, cc = e & 63;
-    if (SC1) {
-      store_sc1(rsrc_of(Aic), (int)(((int64_t)r * lda + cc) * 8), sP[r * LD64 + cc], sP[r * LD64 + cc + 1]);
-    } else {
-      *reinterpret_cast<double2*>(Aic + (int64_t)r * lda + cc) = make_double2(sP[r * LD64 + cc], sP[r * LD64 + cc + 1]);
-    }
+    *reinterpret_cast<double2*>(Aic + (int64_t)r * lda + cc) = make_double2(sP[r * LD64 + cc], sP[r * LD64 + cc + 1]);
   }
 }
 
@@ -425,207 +391,6 @@ __device__ __forceinline__ void lookahead_role(double* __restrict__ A, int64_t l
       for (int r = 0; r < 4; ++r) C[(int64_t)Tile64::row_of(ii, r) * lda + Tile64::col_of(jj)] = -tl.acc[ii][jj][r];
 }
 
-// ---- persistent dataflow schedule (one launch for the whole factorisation) ------------------------------------
-// VERDICT r1 "next 3": the 64 dependent launches of the eager schedule each last as long as their slowest trailing tile
-// (31-46 us in steps 1-22 at n = 4096 against a ~15 us panel chain), plus a launch boundary.  Here ONE launch holds
-//  * nblk panel workgroups: workgroup i runs the panel tasks P(c, i), c = 0 .. i, of its row block in order (exactly
-//    panel_role's work with c0 = c-1: the column c-1 update of tiles (c, c) and (i, c), the in-LDS factorisation, L_ic
-//    stored) and publishes pdone[c][i];
-//  * NT trailing workgroups: the tasks U(c, I, J) = "apply column c to the 128x128 tile (I, J)" for every tile whose
-//    block columns reach c+2, in the order (c, J, I), dealt round robin (task k -> workgroup k mod NT), each bumping
-//    the tile's version counter.
-// Dependencies: P(c, i) waits for pdone[c-1][c] (L_{c,c-1}) and for the versions of the tiles holding (c, c) and
-// (i, c) to reach c-1 (updates 0 .. c-2 applied; its own previous task produced L_{i,c-1}); U(c, I, J) waits for
-// pdone[c][rows 2I, 2I+1, 2J, 2J+1] and for the tile's version to equal c (updates to a tile are applied in column
-// order).  Every task waits only on tasks that precede it in its pool's order or on the other pool's earlier tasks,
-// and the grid is sized to be co-resident (<= 2 workgroups per CU, 75 KB LDS each), so the schedule cannot deadlock;
-// every spin is bounded and gives up (info = -1) rather than hang.
-// Hand-offs follow cdna_hip_programming.md §6 Guideline 16 (R1): payload stores write-through (agent-scope atomic
-// stores), every storing wave drains (s_waitcnt vmcnt(0)), a barrier, then ONE lane stores the flag / version; the
-// consumer polls relaxed from one wave, then ONE agent-scope acquire, vmcnt(0), barrier, plain loads.
-// The arithmetic, and its order, is the eager schedule's: L is bit-identical to the multi-launch path.
-struct SyncWords {
-  int* base;  // nblk * nblk pdone flags, then the 128-tile versions, then the timeout word
-  int nblk;
-  __device__ int* pdone(int c, int i) const { return base + c * nblk + i; }
-  __device__ int* ver(int I, int J) const { return base + nblk * nblk + I * (I + 1) / 2 + J; }
-  __device__ int* timeout() const { const int M = nblk / 2; return base + nblk * nblk + M * (M + 1) / 2; }
-};
-
-__host__ __device__ inline int sync_word_count(int nblk) {
-  const int M = nblk / 2;
-  return nblk * nblk + M * (M + 1) / 2 + 1;
-}
-
-constexpr unsigned kPotrfSpinLimit = 1u << 23;
-
-// One wave polls: lane k waits for *mine >= want (lanes with mine == nullptr are satisfied); the other waves of the
-// workgroup meet it at the barrier that follows the acquire.  Returns false when the timeout word is (or gets) set.
-__device__ __forceinline__ bool poll_ge(const SyncWords& sw, int* mine, int want) {
-  const int lane = threadIdx.x & 63;
-  for (unsigned spins = 0;; ++spins) {
-    bool ok = true;
-    if (mine) ok = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
-    if (__all(ok)) return true;
-    if ((spins & 255) == 255) {
-      if (__hip_atomic_load(sw.timeout(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
-      if (spins >= kPotrfSpinLimit) {
-        if (lane == 0) __hip_atomic_store(sw.timeout(), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return false;
-      }
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// Wave 0 polls (its lanes' words), then the acquire that makes the other workgroups' write-through stores visible to
-// this CU's plain loads, then a barrier for the other waves.  Returns false (uniformly) on timeout.
-__device__ __forceinline__ bool wait_and_acquire(const SyncWords& sw, int* mine, int want) {
-  __shared__ int s_ok;
-  if (threadIdx.x < 64) {
-    const bool ok = poll_ge(sw, mine, want);
-#ifndef GPX_PROBE_NO_ACQUIRE  // timing experiments only (tools/potrf_probe.hip); never defined in the library
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (threadIdx.x == 0) s_ok = ok ? 1 : 0;
-  }
-  __syncthreads();
-  return s_ok != 0;
-}
-
-// Every storing wave drains its write-through stores, a barrier, then one lane publishes `value` into *word.
-__device__ __forceinline__ void publish(int* word, int value) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(word, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// U(c, I, J): tile (I, J) of the 128-grid -= L_{rows, c} L_{cols, c}^T, stored (write-through) for the 64-blocks
-// (rb, cb) with cb >= c+2 and rb >= cb.
-__device__ __forceinline__ void persist_update(double* __restrict__ A, int64_t lda, int c, int I, int J, double* lds) {
-  const int r0 = 2 * I, q0 = 2 * J;
-  const double* Li = A + (int64_t)r0 * NB * lda + (int64_t)c * NB;
-  const double* Lj = A + (int64_t)q0 * NB * lda + (int64_t)c * NB;
-  double* C = A + (int64_t)r0 * NB * lda + (int64_t)q0 * NB;
-  const __amdgpu_buffer_rsrc_t rc = rsrc_of(C);
-  Tile128 tl;
-  // acc = -C, loads issued together with the first k-tile's, then acc += L_i L_j^T: C - L_i L_j^T = -acc, stored with
-  // no load round trip after the k loop (an epilogue that loaded C after the product spent 30-45 us per task waiting
-  // on the Infinity Cache)
-  tl.load_neg_c(C, lda);
-  tl.run_acc(Li, lda, Lj, lda, 0, NB, lds);
-#pragma unroll
-  for (int i = 0; i < Tile128::WM; ++i)
-#pragma unroll
-    for (int j = 0; j < Tile128::WN; ++j) {
-      const int col = Tile128::col_of(j), cb = q0 + (col >> 6);
-      if (cb < c + 2) continue;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = Tile128::row_of(i, r), rb = r0 + (row >> 6);
-        if (rb >= cb) store_sc1(rc, (int)(((int64_t)row * lda + col) * 8), -tl.acc[i][j][r]);
-      }
-    }
-}
-
-// First 128-tile column that U(c, ., .) touches, and its task count.
-__device__ __forceinline__ int ucol0(int c) { return (c + 2) / 2; }
-__device__ __forceinline__ int utasks(int c, int M) {
-  const int m = M - ucol0(c);
-  return m > 0 ? m * (m + 1) / 2 : 0;
-}
-
-__device__ __forceinline__ void persist_panel_loop(double* __restrict__ A, int64_t lda, int nblk, int i,
-                                                double* __restrict__ Dinv, int32_t* __restrict__ info, SyncWords sw,
-                                                double* lds) {
-  // panel workgroup of row block i: P(0, i), P(1, i), ..., P(i, i)
-  __builtin_amdgcn_s_setprio(3);
-  for (int c = 0; c <= i; ++c) {
-    // lane 0: L_{c,c-1} published (its own L_{i,c-1} came from its previous task); lanes 1 / 2: updates 0 .. c-2
-    // applied to the tiles holding (c, c) and (i, c)
-    const int lane = threadIdx.x & 63;
-    int* mine = nullptr;
-    int want = 0;
-    if (c > 0) {
-      if (lane == 0) {
-        mine = sw.pdone(c - 1, c);
-        want = 1;
-      } else if (lane == 1) {
-        mine = sw.ver(c / 2, c / 2);
-        want = c - 1;
-      } else if (lane == 2) {
-        mine = sw.ver(i / 2, c / 2);
-        want = c - 1;
-      }
-    }
-    GPX_PERSIST_STAMP(0, c, i, 0);
-    const bool ok = wait_and_acquire(sw, mine, want);
-    GPX_PERSIST_STAMP(0, c, i, 1);
-    if (!ok && threadIdx.x == 0) atomicCAS(info, 0, -1);
-    if (ok && __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-      panel_role<true>(A, lda, c, i - c, nblk, c > 0 ? c - 1 : 0, Dinv, info, lds);
-    GPX_PERSIST_STAMP(0, c, i, 2);
-    publish(sw.pdone(c, i), 1);
-    GPX_PERSIST_STAMP(0, c, i, 3);
-    __syncthreads();  // LDS reuse by the next task
-  }
-}
-
-__device__ __forceinline__ void persist_trailing_loop(double* __restrict__ A, int64_t lda, int nblk, int tw, int NT,
-                                                   int32_t* __restrict__ info, SyncWords sw, double* lds) {
-  // trailing workgroup: tasks k = tw, tw + NT, ... of the (c, J, I)-ordered list
-  const int M = nblk / 2;
-  int c = 0, base = 0;  // tasks of columns < c
-  for (int k = tw;; k += NT) {
-    while (c < nblk && k >= base + utasks(c, M)) base += utasks(c++, M);
-    if (c >= nblk) break;
-    // decode the task inside column c: J ascending from ucol0(c), then I from J
-    int r = k - base, J = ucol0(c);
-    while (r >= M - J) r -= M - J++;
-    const int I = J + r;
-    // lanes 0-3: L_{r, c} published for the tile's rows 2I, 2I+1 and columns 2J, 2J+1; lane 4: the tile's version = c
-    const int lane = threadIdx.x & 63;
-    int* mine = nullptr;
-    int want = 1;
-    if (lane < 4) mine = sw.pdone(c, lane < 2 ? 2 * I + lane : 2 * J + lane - 2);
-    else if (lane == 4) {
-      mine = sw.ver(I, J);
-      want = c;
-    }
-    GPX_PERSIST_STAMP(1, c, I * 64 + J, 0);
-    const bool ok = wait_and_acquire(sw, mine, want);
-    GPX_PERSIST_STAMP(1, c, I * 64 + J, 1);
-    if (!ok && threadIdx.x == 0) atomicCAS(info, 0, -1);
-    if (ok && __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-      persist_update(A, lda, c, I, J, lds);
-    GPX_PERSIST_STAMP(1, c, I * 64 + J, 2);
-    publish(sw.ver(I, J), c + 1);
-    GPX_PERSIST_STAMP(1, c, I * 64 + J, 3);
-    __syncthreads();
-  }
-}
-
-__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
-potrf_persist_kernel(double* __restrict__ A, int64_t lda, int nblk, int npanel_wg, double* __restrict__ Dinv,
-                     int32_t* __restrict__ info, int* __restrict__ sync, int64_t sa, int64_t sd, int64_t ss) {
-  A += blockIdx.y * sa;  // problem of a batched fit
-  Dinv += blockIdx.y * sd;
-  info += blockIdx.y;
-  const SyncWords sw{sync + blockIdx.y * ss, nblk};
-  __shared__ __attribute__((aligned(16))) double lds[STEP_LDS];
-  const int b = blockIdx.x;
-  if (b < npanel_wg)
-    persist_panel_loop(A, lda, nblk, b, Dinv, info, sw, lds);
-  else
-    persist_trailing_loop(A, lda, nblk, b - npanel_wg, gridDim.x - npanel_wg, info, sw, lds);
-}
-
-__global__ void potrf_sync_clear_kernel(int* __restrict__ sync, int words, int64_t ss) {
-  int* p = sync + blockIdx.y * ss;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < words; e += gridDim.x * blockDim.x) p[e] = 0;
-}
-
 // Work split of launch c.  Flush launches (plan.flush) apply the columns k0 .. c-1 (k0 = the previous flush launch, or 0)
 // to the trailing matrix.  mode 0: the panels apply the pending columns c0 = k0 .. c-1, the flush covers columns >= c+1.
 // mode 1: the panels apply column c-1 only, lookahead workgroups bring column c+1 up to date (columns look_a = k0 ..
@@ -661,15 +426,13 @@ inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush,
 
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
 potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, StepPlan s, double* __restrict__ Dinv,
-                  int32_t* __restrict__ info, int first_wg, int64_t sa, int64_t sd, int prio) {
+                  int32_t* __restrict__ info, int first_wg, int64_t sa, int64_t sd) {
   A += blockIdx.y * sa;  // problem of a batched fit
   Dinv += blockIdx.y * sd;
   info += blockIdx.y;
   if (*(volatile int32_t*)info != 0) return;  // an earlier step failed: leave the rest untouched
   __shared__ __attribute__((aligned(16))) double lds[STEP_LDS];
   const int b = first_wg + (int)blockIdx.x;
-  // the panel is the launch's critical path; its waves share SIMDs with trailing tiles' MFMA streams
-  if (prio && b < s.npanel) __builtin_amdgcn_s_setprio(3);
   if (b >= s.npanel + s.nlook && b < s.tbase) return;  // alignment padding of the trailing workgroups
   const int role = b < s.npanel ? 0 : (b < s.npanel + s.nlook ? 1 : 2);
   GPX_STEP_STAMP(role, c, b, 0);
@@ -722,69 +485,43 @@ __global__ void __launch_bounds__(WG) potrf_dinv_kernel(double* __restrict__ A, 
 
 // Trailing updates are flushed every `lazy` launches (K = 64 lazy per flush): C tiles are read and written once per
 // `lazy` block columns instead of every column, and the panel workgroups apply the (at most `lazy`) pending columns
-// to their own tiles.
-// Measured (tools/lazy_sweep.sh, profiles/r01_potrf_lazy_sweep.log): n = 4096: lazy 1/2 -> potrf 1.73/1.90 ms (the
-// K = 128 panel pre-update sits on the critical path, the trailing update mostly hides under the panel chain);
-// n = 8192: lazy 1/2/4 -> 7.05/6.75/7.21 ms; n = 16384: lazy 1/2/4/8 -> 46.3/37.4/34.3/35.3 ms (the trailing update
-// dominates).  GPX_POTRF_LAZY overrides.
-// Schedule by size (tools/lazy_sweep.sh, profiles/r01_potrf_lazy_sweep*.log):
+// to their own tiles.  Schedule by size (tools/lazy_sweep.sh, profiles/r01_potrf_lazy_sweep*.log):
 //   n = 4096:  mode 0, g = 1 -> potrf 1.73-1.75 ms (mode 1 g = 2/4: 1.81/1.94: a K = 128 flush tile is >= 14 us of
 //              MFMA on one CU, longer than the ~20 us panel window once two share a CU);
 //   n = 8192:  mode 1, g = 4 -> 6.34 ms (mode 0 g = 2: 6.69);
 //   n = 16384: mode 1, g = 8 -> 31.4 ms (mode 0 g = 4: 34.4, g = 1: 46.3).
-// GPX_POTRF_MODE / GPX_POTRF_LAZY override.
-static int env_int(const char* name) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : -1;
-}
-
-static int potrf_lazy(int nblk) {
-  static const int env = env_int("GPX_POTRF_LAZY");
-  if (env > 0) return env > 16 ? 16 : env;
+// The handle options GPX_OPT_POTRF_LAZY / GPX_OPT_POTRF_MODE override.  Flushing every second launch only in the early,
+// trailing-bound launches and panel-wave priority were measured neutral (DESIGN.md §5, items 14 and the prio knob)
+// and are not offered.  Trailing tiles are dealt to the XCDs in 8 x 8 super-block chunks (trail_tile xmap = 1).
+static int potrf_lazy(const Context* ctx, int nblk) {
+  if (ctx->potrf_lazy > 0) return ctx->potrf_lazy;
   return nblk > 128 ? 8 : (nblk > 64 ? 4 : 1);
 }
 
-static int potrf_mode(int nblk) {
-  static const int env = env_int("GPX_POTRF_MODE");
-  if (env == 0 || env == 1) return env;
+static int potrf_mode(const Context* ctx, int nblk) {
+  if (ctx->potrf_mode == 0 || ctx->potrf_mode == 1) return ctx->potrf_mode;
   return nblk > 64 ? 1 : 0;
-}
-
-// Flush interval at launch c: `early_g` for the first `early_end` launches (their trailing update is HBM-bound: the
-// C tiles' read + write per flush, not the MFMAs, set the launch length), then potrf_lazy.  GPX_POTRF_EARLY_G /
-// GPX_POTRF_EARLY_END override (0 = one interval throughout).
-static int potrf_flush_interval(int c, int nblk) {
-  static const int eg = env_int("GPX_POTRF_EARLY_G"), ee = env_int("GPX_POTRF_EARLY_END");
-  const int early_g = eg > 0 ? eg : 0, early_end = ee > 0 ? ee : 0;
-  return (early_g > 0 && c < early_end) ? early_g : potrf_lazy(nblk);
-}
-
-// Trailing tile order (trail_tile): 1 = XCD-chunked 8 x 8 super-blocks, 0 = row-major.  GPX_POTRF_XMAP overrides.
-static int potrf_xmap() {
-  static const int env = env_int("GPX_POTRF_XMAP");
-  return env >= 0 ? env : 1;
 }
 
 // The plan of every launch c < cend (flush launches: c >= 1 and at least one interval after the previous flush).
 template <typename F>
-static void for_each_step(int nblk, int mode, int cend, F&& f) {
+static void for_each_step(const Context* ctx, int nblk, int mode, int cend, F&& f) {
+  const int g = potrf_lazy(ctx, nblk);
   int last = 0;
   for (int c = 0; c < cend; ++c) {
-    const bool flush = c >= 1 && c - last >= potrf_flush_interval(c, nblk);
-    f(c, step_plan(c, nblk, mode, last, flush, potrf_xmap()));
+    const bool flush = c >= 1 && c - last >= g;
+    f(c, step_plan(c, nblk, mode, last, flush, 1));
     if (flush) last = c;
   }
 }
 
 static void launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
                          int cbeg, int cend) {
-  const int mode = potrf_mode(nblk);
-  static const int prio_env = env_int("GPX_POTRF_PRIO");
-  const int prio = prio_env < 0 ? 0 : prio_env;
-  for_each_step(nblk, mode, cend, [&](int c, const StepPlan& s) {
+  const int mode = potrf_mode(ctx, nblk);
+  for_each_step(ctx, nblk, mode, cend, [&](int c, const StepPlan& s) {
     if (c < cbeg) return;
     const dim3 grid(s.tbase + s.ntrail, bt.count);
-    potrf_step_kernel<<<grid, WG, 0, ctx->stream>>>(A, lda, c, nblk, s, Dinv, info, 0, bt.k, bt.dinv, prio);
+    potrf_step_kernel<<<grid, WG, 0, ctx->stream>>>(A, lda, c, nblk, s, Dinv, info, 0, bt.k, bt.dinv);
   });
 }
 
@@ -794,40 +531,13 @@ static void launch_dinv(Context* ctx, int nblk, double* A, int64_t lda, double* 
                                                                       bt.w);
 }
 
-// Persistent schedule: opt-in (GPX_POTRF_PERSIST=1) for 4 <= nblk <= 128 when the panel workgroups plus >= 64
-// trailing workgroups per problem fit in two workgroups per CU.  Measured slower than the multi-launch schedule
-// (n = 4096: 2.52 vs 1.74 ms): in the combined kernel the 128x128 trailing tasks spill (~120 VGPRs) and run
-// ~40 us instead of ~20, and the panel tasks ~22 us instead of ~15, which outweighs the removed launch boundaries.
-static int persist_grid(int nblk, int batch) {
-  static const int env = env_int("GPX_POTRF_PERSIST");
-  if (env != 1 || nblk > 128 || nblk < 4) return 0;
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
-    cus = prop.multiProcessorCount;
-  }
-  const int per = 2 * cus / batch;  // co-resident workgroups per problem
-  return per - nblk >= 64 ? per : 0;
-}
-
 hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
                         double* W, int64_t ldw) {
   LaunchTimer tm(ctx, GPX_TIMER_POTRF);
   const int nblk = npad / NB;
-  const int grid = persist_grid(nblk, bt.count);
-  if (grid) {
-    // the sync words live in the first half of Dinv (written by potrf_dinv only after the factorisation)
-    int* sync = reinterpret_cast<int*>(Dinv);
-    const int words = sync_word_count(nblk);
-    const int64_t ss = 2 * bt.dinv;  // ints per problem
-    potrf_sync_clear_kernel<<<dim3((words + 1023) / 1024, bt.count), 1024 / 4, 0, ctx->stream>>>(sync, words, ss);
-    potrf_persist_kernel<<<dim3(grid, bt.count), WG, 0, ctx->stream>>>(A, lda, nblk, nblk, Dinv, info, sync, bt.k,
-                                                                       bt.dinv, ss);
-  } else {
-    launch_steps(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk);
-  }
+  if (ctx->potrf_schedule != 1 && potrf_dag_workers(ctx, npad, bt.count) > 0)
+    return launch_potrf_dag(ctx, npad, A, lda, Dinv, info, bt, W, ldw);
+  launch_steps(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk);
   launch_dinv(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, W, ldw);
   return hipGetLastError();
 }

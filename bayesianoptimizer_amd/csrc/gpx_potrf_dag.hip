@@ -1,0 +1,980 @@
+// Persistent dataflow Cholesky (lower, NB = 64) for npad <= 4096: ONE launch per factorisation (per batch).
+// SURVEY §8a row a4 (psd_safe_cholesky in GPyTorch's exact path [upstream], reached from
+// optimization/Bayesian.py:89-94); the failing pivot is reported in *info for the jitter retry of
+// optimization/Bayesian6.py:481-488.
+//
+// Why: the multi-launch schedule (gpx_potrf.hip) runs one launch per block column, and every launch lasts as long as its
+// slowest workgroup: at n = 4096 the first ~22 launches are bound by the trailing update (2-3x the ~20 us panel chain)
+// and every launch pays a kernel boundary (3.3-3.9 us).  Here the work is a dataflow graph inside one launch:
+//  * the CHAIN workgroup (blockIdx.x == 0) owns the critical path.  Step c: wait until tiles (c, c-1) and (c, c) hold
+//    every update of columns < c-1, L_{c,c-1} = A_{c,c-1} D_{c-1}^T (D_{c-1} = L_{c-1,c-1}^{-1} is still in its LDS),
+//    A_cc -= L_{c,c-1} L_{c,c-1}^T, then factor A_cc in LDS (four 16-pivot in-wave blocks, gpx_chol64.h) while the other
+//    waves build the full inverse D_c = L_cc^{-1} block row by block row.  L and D leave as write-through stores.
+//  * POOL workgroups take tasks from a host-scheduled list (one atomic ticket per task):
+//      FR(i, k)        L_ik = A_ik D_k^T, then A_{i,k+1} -= L_ik L_{k+1,k}^T     (the next panel column, row i)
+//      U64(i, j, k0, k1)   A_ij -= sum_{k0 <= k < k1} L_ik L_jk^T  on one 64x64 block
+//      U128(I, J, k0, k1)  the same on the 128x128 tile of blocks (2I, 2I+1) x (2J, 2J+1)
+//    Column j receives stage j-1 from FR (the chain for the diagonal block), stage j-2 from U64 "next column" tasks,
+//    and (odd j) stage j-3 from U64 as well; every earlier stage comes from U128 tiles of the 128-column pair j/2, whose
+//    stages are aggregated into K = 64 g products while the pair is far from the front (each C tile read and written
+//    once per g columns instead of every column).
+//  Dependencies are per-block version counters (stages applied), per-row counters of published L_ik and the chain's
+//  progress word.  Hand-offs follow cdna_hip_programming.md §6 Guideline 16 in its sc1 form (MI355X_MICROARCH.md
+//  § visibility, valid-forms table row 1): every handed-off byte is stored with an sc1 (write-through) store, every
+//  storing wave drains (s_waitcnt vmcnt(0)), a workgroup barrier, then ONE lane stores the counter; the consumer's one
+//  wave polls with sc1 loads, a barrier, then EVERY load of handed-off bytes is an sc1 buffer load; one workgroup per
+//  CU (LDS > 80 KB).  Spins are bounded; an abort word (pivot failure or timeout) makes every waiter give up.
+//  The task order is a host simulation's start order (a topological order of the graph), so a task only waits on the
+//  chain or on tasks earlier in the list: with the chain resident and any number of resident pool workgroups the graph
+//  drains.  The arithmetic of every task is fixed (the schedule decides who runs it, never how), so the factor does not
+//  depend on timing or placement and a batched factorisation equals single ones bit for bit.
+#include "gpx_internal.h"
+#include "gpx_device.h"
+#include "gpx_chol64.h"
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <map>
+#include <memory>
+#include <vector>
+
+// Optional timestamp hooks for tools/dag_probe.hip (compiled out in the library).
+#ifndef GPX_DAG_STAMP
+#define GPX_DAG_STAMP(kind, a, b, s)
+#endif
+#ifndef GPX_DAG_TASK_STAMP
+#define GPX_DAG_TASK_STAMP(idx, s)
+#endif
+
+namespace gpx {
+namespace dag {
+
+constexpr int LD = LD64;              // LDS row length of a 64x64 tile (doubles)
+constexpr int TILE_D = NB * LD;       // doubles per LDS tile
+constexpr int HDR = 16;               // sync words before the per-row counters
+enum { W_CHAIN = 0, W_ABORT = 1, W_TICKET_FRONT = 2, W_TICKET_BULK = 3 };
+enum { T_FR = 1, T_U64 = 2, T_U128 = 3 };
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr int kSC1 = 16;  // aux operand of the buffer intrinsics: sc1
+
+__device__ __forceinline__ rsrc_t rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ double2 ld2(rsrc_t r, int off) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSC1);
+  return make_double2(__longlong_as_double(((unsigned long long)v.y << 32) | v.x),
+                      __longlong_as_double(((unsigned long long)v.w << 32) | v.z));
+}
+__device__ __forceinline__ double ld1(rsrc_t r, int off) {
+  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kSC1);
+  return __longlong_as_double(((unsigned long long)v.y << 32) | v.x);
+}
+__device__ __forceinline__ void st2(rsrc_t r, int off, double a, double b) {
+  const unsigned long long x = __double_as_longlong(a), y = __double_as_longlong(b);
+  const u32x4 v = {(unsigned)x, (unsigned)(x >> 32), (unsigned)y, (unsigned)(y >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kSC1);
+}
+__device__ __forceinline__ void st1(rsrc_t r, int off, double a) {
+  const unsigned long long x = __double_as_longlong(a);
+  const u32x2 v = {(unsigned)x, (unsigned)(x >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, kSC1);
+}
+
+struct Sync {
+  int* w;
+  int nblk;
+  __device__ int* chain() const { return w + W_CHAIN; }
+  __device__ int* abort_word() const { return w + W_ABORT; }
+  __device__ int* ticket(int which) const { return w + W_TICKET_FRONT + which; }
+  __device__ int* lrow(int i) const { return w + HDR + i; }
+  __device__ int* ver(int i, int j) const { return w + HDR + nblk + i * nblk + j; }
+};
+
+__host__ __device__ inline int sync_words(int nblk) { return (HDR + nblk + nblk * nblk + 3) & ~3; }
+
+// One wave polls: lane l waits for *mine >= want (mine == nullptr: satisfied).  Returns false once the abort word is set
+// (or this wave sets it after `limit` spins: timeout).
+__device__ __forceinline__ bool wave_wait(const Sync& s, const int* mine, int want, unsigned limit) {
+  const int lane = threadIdx.x & 63;
+  for (unsigned spins = 0;; ++spins) {
+    const bool ok = !mine || __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want;
+    if (__all(ok)) return true;
+    if (spins >= limit) {
+      if (lane == 0) __hip_atomic_store(s.abort_word(), 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    if ((spins & 63) == 63 && __hip_atomic_load(s.abort_word(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+      return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// Workgroup wait: wave 0 polls, every wave leaves through the same barrier (uniform result).  After it, handed-off
+// bytes are read with sc1 loads only.
+__device__ __forceinline__ bool wg_wait(const Sync& s, const int* mine, int want, unsigned limit) {
+  int ok = 1;
+  if (threadIdx.x < 64) ok = wave_wait(s, mine, want, limit) ? 1 : 0;
+  return __syncthreads_and(ok) != 0;
+}
+
+// Every storing wave drains its sc1 stores, a barrier, then lanes 0 .. nw-1 of wave 0 store their word.
+__device__ __forceinline__ void wg_publish(int* word, int value) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0 && word) __hip_atomic_store(word, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// 64x64 tile (row-major, leading dimension ld) -> LDS (row length LD), sc1 loads, all issued before the LDS writes.
+__device__ __forceinline__ void tile_in(const double* G, int64_t ld, double* S) {
+  const rsrc_t r = rsrc(G);
+  const int t = threadIdx.x;
+  double2 v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = (t + q * WG) * 2, rr = e >> 6, cc = e & 63;
+    v[q] = ld2(r, (int)(((int64_t)rr * ld + cc) * 8));
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = (t + q * WG) * 2, rr = e >> 6, cc = e & 63;
+    S[rr * LD + cc] = v[q].x;
+    S[rr * LD + cc + 1] = v[q].y;
+  }
+}
+
+// LDS tile -> global (sc1); LOWER: 16-blocks above the block diagonal stored as zeros.
+template <bool LOWER>
+__device__ __forceinline__ void tile_out(const double* S, double* G, int64_t ld) {
+  const rsrc_t r = rsrc(G);
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int e = (t + q * WG) * 2, rr = e >> 6, cc = e & 63;
+    double a = S[rr * LD + cc], b = S[rr * LD + cc + 1];
+    if (LOWER && (cc >> 4) > (rr >> 4)) a = b = 0.0;
+    st2(r, (int)(((int64_t)rr * ld + cc) * 8), a, b);
+  }
+}
+
+// Block row w (16 rows) of R = S D^T, D lower triangular (64x64 in LDS): acc[bj] = R(16w.., 16bj..).  The four
+// accumulation chains are interleaved per k-step (they share the A operand), so consecutive MFMAs are independent.
+__device__ __forceinline__ void rowblock_times_lower_t(d4 (&acc)[4], const double* S, const double* D, int w) {
+  const int lane = threadIdx.x & 63, m = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int bj = 0; bj < 4; ++bj) acc[bj] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) {
+    const double a = S[(16 * w + m) * LD + 4 * ks + kk];
+#pragma unroll
+    for (int bj = 0; bj < 4; ++bj)
+      if (ks < 4 * (bj + 1)) acc[bj] = mfma16x16x4(a, D[(16 * bj + m) * LD + 4 * ks + kk], acc[bj]);
+  }
+}
+
+// Block row w of C - R Q^T (64x64 operands in LDS, full K = 64), four chains interleaved: acc[bj] = C(16w.., 16bj..)
+// - sum_k R(16w + ., k) Q(16bj + ., k).
+__device__ __forceinline__ void rowblock_sub_abt(d4 (&acc)[4], const double* C, const double* R, const double* Q, int w) {
+  const int lane = threadIdx.x & 63, m = lane & 15, kk = lane >> 4;
+#pragma unroll
+  for (int bj = 0; bj < 4; ++bj) acc[bj] = load_block16(C, 16 * w, 16 * bj);
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) {
+    const double a = -R[(16 * w + m) * LD + 4 * ks + kk];
+#pragma unroll
+    for (int bj = 0; bj < 4; ++bj) acc[bj] = mfma16x16x4(a, Q[(16 * bj + m) * LD + 4 * ks + kk], acc[bj]);
+  }
+}
+
+// Blocks (I0,J0), (I1,J1), (I2,J2) of A -= L L^T (K = 64, L in LDS), three chains interleaved.
+template <int I0, int J0, int I1, int J1, int I2, int J2>
+__device__ __forceinline__ void syrk3(double* sA, const double* L) {
+  const int lane = threadIdx.x & 63, m = lane & 15, kk = lane >> 4;
+  d4 c0 = load_block16(sA, 16 * I0, 16 * J0), c1 = load_block16(sA, 16 * I1, 16 * J1),
+     c2 = load_block16(sA, 16 * I2, 16 * J2);
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) {
+    const int k = 4 * ks + kk;
+    c0 = mfma16x16x4(-L[(16 * I0 + m) * LD + k], L[(16 * J0 + m) * LD + k], c0);
+    c1 = mfma16x16x4(-L[(16 * I1 + m) * LD + k], L[(16 * J1 + m) * LD + k], c1);
+    c2 = mfma16x16x4(-L[(16 * I2 + m) * LD + k], L[(16 * J2 + m) * LD + k], c2);
+  }
+  store_block16(sA, 16 * I0, 16 * J0, c0);
+  store_block16(sA, 16 * I1, 16 * J1, c1);
+  store_block16(sA, 16 * I2, 16 * J2, c2);
+}
+
+template <int I0, int J0>
+__device__ __forceinline__ void syrk1(double* sA, const double* L) {
+  const int lane = threadIdx.x & 63, m = lane & 15, kk = lane >> 4;
+  d4 c0 = load_block16(sA, 16 * I0, 16 * J0);
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) {
+    const int k = 4 * ks + kk;
+    c0 = mfma16x16x4(-L[(16 * I0 + m) * LD + k], L[(16 * J0 + m) * LD + k], c0);
+  }
+  store_block16(sA, 16 * I0, 16 * J0, c0);
+}
+
+// A -= L L^T on the ten lower / diagonal 16-blocks of a 64x64 tile (both in LDS), three blocks per wave at most
+__device__ __forceinline__ void syrk_lower(double* sA, const double* L, int w) {
+  if (w == 0) syrk3<0, 0, 1, 0, 1, 1>(sA, L);
+  else if (w == 1) syrk3<2, 0, 2, 1, 2, 2>(sA, L);
+  else if (w == 2) syrk3<3, 0, 3, 1, 3, 2>(sA, L);
+  else syrk1<3, 3>(sA, L);
+}
+
+// acc (block row w of a 64x64 result, acc layout) -> global tile G (sc1, 8-byte stores) and, optionally, LDS S.
+__device__ __forceinline__ void rowblock_out(const d4 (&acc)[4], int w, double* G, int64_t ld, double* S) {
+  const rsrc_t r = rsrc(G);
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = 16 * w + (lane >> 4) + 4 * q, col = 16 * bj + (lane & 15);
+      st1(r, (int)(((int64_t)row * ld + col) * 8), acc[bj][q]);
+      if (S) S[row * LD + col] = acc[bj][q];
+    }
+}
+
+// ---- one step of the chain ---------------------------------------------------------------------------------------
+// In: sA = A_cc and (c > 0) sB = A_{c,c-1}, both holding every update of columns < c-1; sX = D_{c-1}.
+//  (c > 0) S: every wave computes its block row of L_{c,c-1} = A_{c,c-1} D_{c-1}^T into sB and global memory (sc1).
+//      Wave 0 then applies A_00 -= L_0 L_0^T (its own rows only) and goes straight into the first pivot block; waves
+//      1-3 wait for the four L block rows (LDS counter) and apply the nine other blocks of A_cc -= L L^T while it runs.
+//  Pivot block s (0..3): wave 0 factors + inverts block (s, s) in registers (chol16), then - without a barrier - the
+//      T and U items of block row s+1 and the next pivot block; waves 1-3 do the other T items (L_is = A_is D_ss^T),
+//      the U items (A_ij -= L_is L_js^T) and block row s of the inverse, X_sj = -D_ss sum_{k=j}^{s-1} L_sk X_kj.
+//  After pivot blocks 1 and 2, waves 1-3 look (one poll) whether the next step's tiles (c+1, c) and (c+1, c+1) are
+//      final through column c-1 and, once they are, load them into sB / sN (the 64 x 128 strip, one third per wave).
+// Out: sA = L_cc (lower 16-blocks), sX = D_c.  Returns the failing pivot 0..63 or -1, uniform; *pref == 3: prefetched.
+struct ChainShared {
+  int cnt, srow, fail, pref, prefdone;
+};
+
+__device__ __forceinline__ void prefetch_share(const double* strip, int64_t ld, double* sB, double* sN, int w) {
+  const int lane = threadIdx.x & 63;
+  const rsrc_t r = rsrc(strip);
+  const int col = 2 * lane;  // 0 .. 126 over the 128 columns of the strip
+  double* dst = col < NB ? sB : sN;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    double2 v[11];
+#pragma unroll
+    for (int q = 0; q < 11; ++q) {
+      const int row = (w - 1) + 3 * (11 * half + q);
+      if (row < NB) v[q] = ld2(r, (int)(((int64_t)row * ld + col) * 8));
+    }
+#pragma unroll
+    for (int q = 0; q < 11; ++q) {
+      const int row = (w - 1) + 3 * (11 * half + q);
+      if (row < NB) {
+        dst[row * LD + (col & 63)] = v[q].x;
+        dst[row * LD + (col & 63) + 1] = v[q].y;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ int chain_step(const Sync& s, int c, int nblk, double* A, int64_t lda, double* sA,
+                                          double* sB, double* sX, double* sN, ChainShared& sh) {
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  auto dblk = [&](int q) { return sX + 16 * q * LD + 16 * q; };
+  auto tsolve = [&](int i, int q) {
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    acc = mfma_lds16<true, LD>(acc, sA, 16 * i, 16 * q, dblk(q), 0, 0, 16, 1.0);
+    store_block16(sA, 16 * i, 16 * q, acc);
+  };
+  auto update = [&](int i, int j, int q) {
+    d4 acc = load_block16(sA, 16 * i, 16 * j);
+    acc = mfma_lds16<true>(acc, sA, 16 * i, 16 * q, sA, 16 * q, 16 * j, 16, -1.0);
+    store_block16(sA, 16 * i, 16 * j, acc);
+  };
+  auto xitem = [&](int q, int j) {
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int k = j; k < q; ++k) acc = mfma_lds16<false>(acc, sA, 16 * q, 16 * k, sX, 16 * k, 16 * j, 16, 1.0);
+    // X_qj = -D_qq acc: the accumulator register r is the B operand of k-step r (rows 4r + lane/16)
+    const int m = lane & 15, kk = lane >> 4;
+    d4 x = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x = mfma16x16x4(-dblk(q)[m * LD + 4 * r + kk], acc[r], x);
+    store_block16(sX, 16 * q, 16 * j, x);
+  };
+  auto lds_add = [&](int* word) {
+    if (lane == 0) __hip_atomic_fetch_add(word, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  auto lds_wait = [&](int* word, int want) {
+    while (__hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want) __builtin_amdgcn_s_sleep(1);
+  };
+  const bool has_next = c + 1 < nblk;
+  const double* strip = A + (int64_t)(c + 1) * NB * lda + (int64_t)c * NB;  // tiles (c+1, c) | (c+1, c+1)
+  bool my_pref = false;
+  auto try_prefetch = [&]() {  // waves 1-3 only
+    if (!has_next || my_pref) return;
+    if (w == 1 && __hip_atomic_load(&sh.pref, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) {
+      const int* mine = lane == 0 ? s.ver(c + 1, c) : (lane == 1 ? s.ver(c + 1, c + 1) : nullptr);
+      const bool ok = !mine || __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= c;
+      if (__all(ok) && lane == 0) __hip_atomic_store(&sh.pref, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (__hip_atomic_load(&sh.pref, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 1) {
+      prefetch_share(strip, lda, sB, sN, w);
+      my_pref = true;
+      lds_add(&sh.prefdone);
+    }
+  };
+  if (t == 0) {
+    sh.cnt = 0;
+    sh.srow = 0;
+    sh.fail = -1;
+    sh.pref = 0;
+    sh.prefdone = 0;
+  }
+  __syncthreads();
+  if (c > 0) {
+    d4 acc[4];
+    rowblock_times_lower_t(acc, sB, sX, w);  // reads only this wave's rows of sB
+    rowblock_out(acc, w, A + (int64_t)c * NB * lda + (int64_t)(c - 1) * NB, lda, sB);
+    GPX_DAG_STAMP(0, c, 0, 1);
+    lds_add(&sh.srow);
+    if (w == 0) {
+      d4 u = load_block16(sA, 0, 0);
+      u = mfma_lds16<true>(u, sB, 0, 0, sB, 0, 0, NB, -1.0);
+      store_block16(sA, 0, 0, u);
+      lds_wait(&sh.srow, 4);  // every wave's S reads of D_{c-1} are done before chol16 overwrites sX
+      GPX_DAG_STAMP(0, c, 0, 2);
+    } else {
+      lds_wait(&sh.srow, 4);
+      if (w == 1) syrk3<1, 0, 2, 1, 3, 1>(sA, sB);
+      else if (w == 2) syrk3<1, 1, 2, 2, 3, 2>(sA, sB);
+      else syrk3<2, 0, 3, 0, 3, 3>(sA, sB);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // L_{c,c-1} drained before the first barrier (published after it)
+  }
+  int fail = -1;
+  for (int q = 0; q < 4; ++q) {
+    if (w == 0) {
+      const int f = chol16<LD>(sA, dblk(q), 16 * q);
+      if (f >= 0 && fail < 0) fail = 16 * q + f;
+    }
+    __syncthreads();  // L_qq, D_qq (q = 0: also A_cc -= L L^T and the stores of L_{c,c-1})
+    GPX_DAG_STAMP(0, c, 0, 3 + q);
+    if (q == 0 && c > 0 && t == 64)
+      __hip_atomic_store(s.chain(), 2 * c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (w == 0) {
+      if (q < 3) tsolve(q + 1, q);
+      lds_add(&sh.cnt);
+      if (q < 3) update(q + 1, q + 1, q);
+    } else {
+      for (int i = q + 1 + w; i < 4; i += 3) tsolve(i, q);
+      lds_add(&sh.cnt);
+      lds_wait(&sh.cnt, 4 * (q + 1));
+      int e = 0;
+      for (int j = q + 1; j < 4; ++j)
+        for (int i = j; i < 4; ++i) {
+          if (i == q + 1 && j == q + 1) continue;  // wave 0's lookahead item
+          if (1 + e % 3 == w) update(i, j, q);
+          ++e;
+        }
+      for (int j = 0; j < q; ++j)
+        if (1 + j % 3 == w) xitem(q, j);
+      if (q == 1 || q == 2) try_prefetch();
+    }
+  }
+  if (t == 0) sh.fail = fail;
+  __syncthreads();
+  GPX_DAG_STAMP(0, c, 0, 7);
+  return sh.fail;
+}
+
+// ---- tile GEMM tasks from global memory (sc1 operand loads) -------------------------------------------------------
+template <int TM>
+struct DagTile : MfmaTile<TM, TM, 16, false, false> {
+  using Base = MfmaTile<TM, TM, 16, false, false>;
+  // operands: rows of A (rsrc at the tile's first row) x k, rows of B x k; element (m, k) at m * ld + k
+  __device__ __forceinline__ void load_sc1(rsrc_t a, rsrc_t b, int64_t ld, int k0) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < Base::A_LOADS; ++q) {
+      const int e = (t + q * WG) * 2, mm = e / 16, kk = e % 16;
+      this->ra[q] = ld2(a, (int)(((int64_t)mm * ld + k0 + kk) * 8));
+    }
+#pragma unroll
+    for (int q = 0; q < Base::B_LOADS; ++q) {
+      const int e = (t + q * WG) * 2, nn = e / 16, kk = e % 16;
+      this->rb[q] = ld2(b, (int)(((int64_t)nn * ld + k0 + kk) * 8));
+    }
+  }
+  __device__ __forceinline__ void load_neg_c_sc1(rsrc_t c, int64_t ld) {
+#pragma unroll
+    for (int i = 0; i < Base::WM; ++i)
+#pragma unroll
+      for (int j = 0; j < Base::WN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          this->acc[i][j][r] = -ld1(c, (int)(((int64_t)Base::row_of(i, r) * ld + Base::col_of(j)) * 8));
+  }
+  __device__ __forceinline__ void run_acc_sc1(rsrc_t a, rsrc_t b, int64_t ld, int kbeg, int kend, double* smem) {
+    double* cur = smem;
+    double* nxt = smem + 16 * (Base::PA + Base::PB);
+    load_sc1(a, b, ld, kbeg);
+    this->store_lds(cur, cur + 16 * Base::PA);
+    __syncthreads();
+    for (int k0 = kbeg; k0 < kend; k0 += 16) {
+      const bool more = (k0 + 16) < kend;
+      if (more) load_sc1(a, b, ld, k0 + 16);
+      this->compute(cur, cur + 16 * Base::PA);
+      if (more) this->store_lds(nxt, nxt + 16 * Base::PA);
+      __syncthreads();
+      double* tmp = cur;
+      cur = nxt;
+      nxt = tmp;
+    }
+  }
+  // C - A B^T = -acc, stored (sc1) where the element's global 16-block is on or below the block diagonal
+  __device__ __forceinline__ void store_lower(rsrc_t c, int64_t ld, int row0, int col0) {
+#pragma unroll
+    for (int i = 0; i < Base::WM; ++i)
+#pragma unroll
+      for (int j = 0; j < Base::WN; ++j) {
+        const int col = Base::col_of(j);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = Base::row_of(i, r);
+          if (((row0 + row) >> 4) >= ((col0 + col) >> 4))
+            st1(c, (int)(((int64_t)row * ld + col) * 8), -this->acc[i][j][r]);
+        }
+      }
+  }
+};
+
+// ---- roles ---------------------------------------------------------------------------------------------------------
+struct Args {
+  double* A;
+  int64_t lda;
+  int nblk;
+  double* Dinv;
+  int32_t* info;
+  double* W;
+  int64_t ldw;
+  int* sync;
+  int64_t sa, sd, sw, ss;  // per-problem strides (A, Dinv, W in doubles; sync in ints)
+  const unsigned long long* tasks;  // front tasks [0, nfront), bulk tasks [nfront, ntasks)
+  int ntasks, nfront, front_workers;
+  unsigned spin_limit;
+};
+
+__device__ void chain_role(const Args& g, double* A, double* Dinv, double* W, int32_t* info, const Sync& s,
+                           double* lds) {
+  double* sA = lds;
+  double* sB = lds + TILE_D;
+  double* sX = lds + 2 * TILE_D;
+  double* sN = lds + 3 * TILE_D;
+  __shared__ ChainShared sh;
+  const int t = threadIdx.x;
+  const int64_t lda = g.lda;
+  const int nblk = g.nblk;
+  auto blk = [&](int i, int j) { return A + (int64_t)i * NB * lda + (int64_t)j * NB; };
+  tile_in(blk(0, 0), lda, sA);
+  __syncthreads();
+  for (int c = 0; c < nblk; ++c) {
+    GPX_DAG_STAMP(0, c, 0, 0);
+    const int f = chain_step(s, c, nblk, A, lda, sA, sB, sX, sN, sh);
+    if (f >= 0) {
+      if (t == 0) {
+        atomicCAS(info, 0, c * NB + f + 1);
+        __hip_atomic_store(s.abort_word(), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      break;
+    }
+    tile_out<true>(sA, blk(c, c), lda);
+    tile_out<true>(sX, Dinv + (int64_t)c * NB * NB, NB);
+    if (W) {  // what potrf_dinv does for a fit with an inverse: W_cc = D_c^T, the lower block of an odd 128-tile zeroed
+      double* Wcc = W + (int64_t)c * NB * g.ldw + (int64_t)c * NB;
+      for (int e = t; e < NB * NB; e += WG) {
+        const int r = e >> 6, cc = e & 63;
+        Wcc[(int64_t)r * g.ldw + cc] = ((r >> 4) > (cc >> 4)) ? 0.0 : sX[cc * LD + r];
+      }
+      if (c & 1) {
+        double* Z = W + (int64_t)c * NB * g.ldw + (int64_t)(c - 1) * NB;
+        for (int e = t; e < NB * NB; e += WG) Z[(int64_t)(e >> 6) * g.ldw + (e & 63)] = 0.0;
+      }
+    }
+    wg_publish(t == 0 ? s.chain() : nullptr, 2 * c + 2);
+    GPX_DAG_STAMP(0, c, 0, 8);
+    if (c + 1 < nblk) {
+      if (sh.prefdone < 3) {  // the next tiles were not final during the factorisation: wait, then load them
+        const int lane = t & 63;
+        const int* mine = lane == 0 ? s.ver(c + 1, c) : (lane == 1 ? s.ver(c + 1, c + 1) : nullptr);
+        if (!wg_wait(s, mine, c, g.spin_limit)) break;
+        tile_in(blk(c + 1, c), lda, sB);
+        tile_in(blk(c + 1, c + 1), lda, sN);
+      }
+      __syncthreads();
+      GPX_DAG_STAMP(0, c, 0, 9);
+      double* tmp = sA;
+      sA = sN;
+      sN = tmp;
+    }
+  }
+}
+
+// The front columns of stage k: k+1 and k+2, and k+3 when k is even (column k+3 odd: its 128-column pair leaves the
+// bulk tiles one stage before its first column does).  Every other (column, stage) update is a bulk U128 tile.
+__host__ __device__ inline int front_cols(int k, int nblk, int (&cols)[3]) {
+  int n = 0;
+  for (int j = k + 1; j <= k + 3 && j < nblk; ++j)
+    if (j < k + 3 || !(k & 1)) cols[n++] = j;
+  return n;
+}
+
+// FR(i, k): L_ik = A_ik D_k^T (published as soon as it is stored), then row i of stage k on the front columns j <= i:
+// the diagonal block first when i is one of them (A_ii -= L_ik L_ik^T needs no other task), then A_ij -= L_ik L_jk^T
+// with L_{k+1,k} from the chain and L_{k+2,k} / L_{k+3,k} from FR(k+2, k) / FR(k+3, k).  One task per row and stage
+// (L_ik stays in LDS for every product), so the chain's next tiles (c+1, c) and (c+1, c+1) come from ONE task,
+// FR(c+1, c-1): one hand-off on the cycle chain -> pool -> chain.
+__device__ bool task_fr(const Args& g, double* A, double* Dinv, const Sync& s, int i, int k, double* lds, int idx) {
+  double* sA = lds;
+  double* sB = lds + TILE_D;
+  double* sX = lds + 2 * TILE_D;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int64_t lda = g.lda;
+  auto blk = [&](int a, int b) { return A + (int64_t)a * NB * lda + (int64_t)b * NB; };
+  int cols[3];
+  const int ncol = front_cols(k, g.nblk, cols);
+  {
+    // lane 0: D_k published; lane 1: A_ik final through column k-1; lanes 2..: the front blocks of row i at stage k
+    const int* mine = nullptr;
+    int want = k;
+    if (lane == 0) {
+      mine = s.chain();
+      want = 2 * k + 2;
+    } else if (lane == 1) {
+      mine = s.ver(i, k);
+    } else if (lane < 2 + ncol && cols[lane - 2] <= i) {
+      mine = s.ver(i, cols[lane - 2]);
+    }
+    if (!wg_wait(s, mine, want, g.spin_limit)) return false;
+  }
+  GPX_DAG_TASK_STAMP(idx, 2);
+  tile_in(blk(i, k), lda, sA);
+  tile_in(Dinv + (int64_t)k * NB * NB, NB, sX);
+  __syncthreads();
+  d4 acc[4];
+  rowblock_times_lower_t(acc, sA, sX, w);
+  rowblock_out(acc, w, blk(i, k), lda, sA);
+  wg_publish(t == 0 ? s.lrow(i) : nullptr, k + 1);
+  GPX_DAG_TASK_STAMP(idx, 3);
+  // the diagonal block first (no wait), then the columns in order
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int q = 0; q < ncol; ++q) {
+      const int j = cols[q];
+      if (j > i || (pass == 0) != (j == i)) continue;
+      tile_in(blk(i, j), lda, sB);
+      if (j == i) {
+        __syncthreads();
+        syrk_lower(sB, sA, w);
+        __syncthreads();
+        tile_out<true>(sB, blk(i, i), lda);
+      } else {
+        const int* mine = lane == 0 ? (j == k + 1 ? s.chain() : s.lrow(j)) : nullptr;
+        if (!wg_wait(s, mine, j == k + 1 ? 2 * k + 3 : k + 1, g.spin_limit)) return false;
+        tile_in(blk(j, k), lda, sX);
+        __syncthreads();
+        rowblock_sub_abt(acc, sB, sA, sX, w);
+        rowblock_out(acc, w, blk(i, j), lda, nullptr);
+      }
+      wg_publish(t == 0 ? s.ver(i, j) : nullptr, k + 1);
+    }
+  }
+  GPX_DAG_TASK_STAMP(idx, 4);
+  return true;
+}
+
+// A_ij -= sum_{k0 <= k < k1} L_ik L_jk^T on a 64x64 block (T = 64) or the 128x128 tile of blocks (2i.., 2j..) (T = 128)
+template <int T>
+__device__ bool task_update(const Args& g, double* A, const Sync& s, int i, int j, int k0, int k1, double* lds,
+                            int idx) {
+  constexpr int R = T / NB;  // 64-blocks per tile side
+  const int lane = threadIdx.x & 63;
+  const int64_t lda = g.lda;
+  const int rb = R * i, cb = R * j;  // first 64-block row / column
+  {
+    // lanes 0 .. 2R-1: L rows published through stage k1-1; lanes 2R ..: the tile's blocks at version k0
+    const int* mine = nullptr;
+    int want = k1;
+    if (lane < R) mine = s.lrow(rb + lane);
+    else if (lane < 2 * R) mine = s.lrow(cb + lane - R);
+    else if (lane < 2 * R + R * R) {
+      const int q = lane - 2 * R, bi = rb + q / R, bj = cb + q % R;
+      if (bi >= bj) mine = s.ver(bi, bj);
+      want = k0;
+    }
+    if (!wg_wait(s, mine, want, g.spin_limit)) return false;
+  }
+  GPX_DAG_TASK_STAMP(idx, 2);
+  const rsrc_t ra = rsrc(A + (int64_t)rb * NB * lda), rbv = rsrc(A + (int64_t)cb * NB * lda);
+  const rsrc_t rc = rsrc(A + (int64_t)rb * NB * lda + (int64_t)cb * NB);
+  DagTile<T> tl;
+  tl.load_neg_c_sc1(rc, lda);
+  tl.run_acc_sc1(ra, rbv, lda, k0 * NB, k1 * NB, lds);
+  tl.store_lower(rc, lda, rb * NB, cb * NB);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x < R * R) {
+    const int bi = rb + threadIdx.x / R, bj = cb + threadIdx.x % R;
+    if (bi >= bj) __hip_atomic_store(s.ver(bi, bj), k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return true;
+}
+
+__device__ void pool_role(const Args& g, double* A, double* Dinv, const Sync& s, double* lds) {
+  __shared__ int s_ticket;
+  // front workers (blockIdx.x 1 .. front_workers) take the front list, then join the bulk list
+  int which = ((int)blockIdx.x <= g.front_workers && g.nfront > 0) ? 0 : 1;
+  for (;;) {
+    if (threadIdx.x == 0)
+      s_ticket = __hip_atomic_fetch_add(s.ticket(which), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    int idx = s_ticket;
+    __syncthreads();
+    if (which == 0) {
+      if (idx >= g.nfront) {
+        which = 1;
+        continue;
+      }
+    } else {
+      idx += g.nfront;
+      if (idx >= g.ntasks) return;
+    }
+    const unsigned long long code = g.tasks[idx];
+    const int type = (int)(code & 0xff), a = (int)((code >> 8) & 0xff), b = (int)((code >> 16) & 0xff),
+              k0 = (int)((code >> 24) & 0xff), k1 = (int)((code >> 32) & 0xff);
+    GPX_DAG_TASK_STAMP(idx, 0);
+    bool ok;
+    if (type == T_FR)
+      ok = task_fr(g, A, Dinv, s, a, b, lds, idx);
+    else if (type == T_U64)
+      ok = task_update<64>(g, A, s, a, b, k0, k1, lds, idx);
+    else
+      ok = task_update<128>(g, A, s, a, b, k0, k1, lds, idx);
+    GPX_DAG_TASK_STAMP(idx, 1);
+    if (!ok) return;
+    __syncthreads();  // LDS reuse by the next task
+  }
+}
+
+// LDS: four 64x64 tiles (the chain's A_cc, L / A_{c,c-1}, D and the next A_cc; a task's operands); > 80 KB, so one
+// workgroup per CU.
+constexpr int LDS_DOUBLES = 4 * TILE_D;
+static_assert(LDS_DOUBLES >= DagTile<128>::LDS_DOUBLES, "U128 staging fits the task LDS");
+static_assert(LDS_DOUBLES * 8 > 80 * 1024, "one workgroup per CU");
+
+__global__ void __launch_bounds__(WG, 1) potrf_dag_kernel(Args g) {
+  const int prob = blockIdx.y;
+  double* A = g.A + prob * g.sa;
+  double* Dinv = g.Dinv + prob * g.sd;
+  double* W = g.W ? g.W + prob * g.sw : nullptr;
+  int32_t* info = g.info + prob;
+  const Sync s{g.sync + prob * g.ss, g.nblk};
+  __shared__ __attribute__((aligned(16))) double lds[LDS_DOUBLES];
+  if (blockIdx.x == 0)
+    chain_role(g, A, Dinv, W, info, s, lds);
+  else
+    pool_role(g, A, Dinv, s, lds);
+  // a timed-out wait leaves the abort word at 2: every workgroup that saw it reports the distinct failure code
+  if (threadIdx.x == 0 && __hip_atomic_load(s.abort_word(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 2)
+    atomicCAS(info, 0, (int32_t)GPX_INFO_TIMEOUT);
+}
+
+// ---- host: the task lists -----------------------------------------------------------------------------------------
+// Two lists: the FRONT (FR and the U64 column tasks, in stage order) for F dedicated front workers, so that the tasks
+// the chain waits on never queue behind long bulk tiles, and the BULK (U128 tiles) for the other workers (front workers
+// join it once the front list is exhausted).  The bulk order is the start order of a discrete-time simulation with
+// measured task durations (microseconds on MI355X at n = 4096, tools/dag_probe): a free bulk worker takes the ready
+// tile with the least slack (deadline = the chain reaching the stage at which its 128-column pair leaves the bulk,
+// minus its remaining work), with every released stage up to kMaxChunk at once, and only when at least kMinChunk
+// stages are released or its slack is short.  F is the simulated best of a few splits.  Any start order of the graph
+// is a topological order, which is all the device relies on (tools/dag_plan_check.hip: every list drains under a
+// worst-case in-order executor, for any number of workers).
+struct Plan {
+  std::vector<unsigned long long> list;  // front tasks, then bulk tasks
+  int nfront = 0, front_workers = 0;
+  unsigned long long* dev = nullptr;
+  double sim_us = 0.0;
+  std::vector<double> sim_chain;  // simulated start of each chain step (diagnostics)
+};
+
+static unsigned long long encode(int type, int a, int b, int k0, int k1) {
+  return (unsigned long long)type | ((unsigned long long)a << 8) | ((unsigned long long)b << 16) |
+         ((unsigned long long)k0 << 24) | ((unsigned long long)k1 << 32);
+}
+
+struct SimCost {
+  double chain = 16.0;    // one chain step
+  double chain_s = 5.0;   // step start -> L_{c,c-1} published
+  double hop = 2.0;       // publish -> visible to a polling workgroup
+  double fr_s = 5.0;      // FR: start -> L_ik published
+  double fr_u = 3.0;      // FR: one front block (tile load + 64x64x64 product + store + publish)
+  double u64(int K) const { return 4.0 + 2.0 * K; }
+  double u128(int K) const { return 6.0 + 10.0 * K; }
+};
+
+static Plan simulate(int nblk, int P, int F) {
+  const SimCost cost;
+  const int kMinChunk = 4, kMaxChunk = 8;
+  const double dt = 0.25, INF = 1e30;
+  Plan plan;
+  plan.front_workers = F;
+  const int M = nblk / 2;
+  std::vector<double> verT((size_t)nblk * nblk * (nblk + 1), INF), lrowT((size_t)nblk * (nblk + 1), INF),
+      chainT(2 * nblk + 2, INF);
+  auto VT = [&](int i, int j, int v) -> double& { return verT[((size_t)i * nblk + j) * (nblk + 1) + v]; };
+  auto LT = [&](int i, int v) -> double& { return lrowT[(size_t)i * (nblk + 1) + v]; };
+  for (int i = 0; i < nblk; ++i) {
+    LT(i, 0) = 0.0;
+    for (int j = 0; j <= i; ++j) VT(i, j, 0) = 0.0;
+  }
+  chainT[0] = 0.0;
+  struct FTask { int type, i, j, k; };
+  std::vector<FTask> front;
+  for (int k = 0; k + 2 < nblk; ++k)
+    for (int i = k + 2; i < nblk; ++i) front.push_back({T_FR, i, k, k});
+  for (const FTask& f : front) plan.list.push_back(encode(T_FR, f.i, f.k, 0, 0));
+  plan.nfront = (int)front.size();
+  size_t fnext = 0;
+  struct BTile { int I, J, v; bool busy; };
+  std::vector<BTile> tiles;
+  for (int J = 2; J < M; ++J)
+    for (int I = J; I < M; ++I) tiles.push_back({I, J, 0, false});
+  size_t bulk_left = tiles.size();
+  int cstep = 0;
+  double cfree = 0.0;
+  struct Worker { double free; int held; bool front; };  // held: front task waiting to start, or -1
+  std::vector<Worker> wk(P);
+  for (int p = 0; p < P; ++p) wk[p] = {0.0, -1, p < F};
+  struct Ev { double t; int kind, a, b, v; };  // kind 0 chain word, 1 lrow, 2 version, 3 tile free
+  std::vector<Ev> evs;
+  auto front_ready = [&](const FTask& f, double now) {
+    int cols[3];
+    const int nc = front_cols(f.k, nblk, cols);
+    bool ok = chainT[2 * f.k + 2] <= now && VT(f.i, f.k, f.k) <= now && chainT[2 * f.k + 3] < INF;
+    for (int q = 0; q < nc; ++q)
+      if (cols[q] <= f.i) ok = ok && VT(f.i, cols[q], f.k) <= now;
+    return ok;
+  };
+  double now = 0.0;
+  for (long guard = 0; guard < 8000000; ++guard, now += dt) {
+    for (size_t e = 0; e < evs.size();) {
+      const Ev x = evs[e];
+      if (x.t > now) {
+        ++e;
+        continue;
+      }
+      if (x.kind == 0) chainT[x.v] = std::min(chainT[x.v], x.t);
+      else if (x.kind == 1) LT(x.a, x.v) = std::min(LT(x.a, x.v), x.t);
+      else if (x.kind == 2) VT(x.a, x.b, x.v) = std::min(VT(x.a, x.b, x.v), x.t);
+      else tiles[x.a].busy = false;
+      evs[e] = evs.back();
+      evs.pop_back();
+    }
+    if (cstep < nblk && cfree <= now &&
+        (cstep == 0 || (VT(cstep, cstep - 1, cstep - 1) <= now && VT(cstep, cstep, cstep - 1) <= now))) {
+      if (cstep) evs.push_back({now + cost.chain_s + cost.hop, 0, 0, 0, 2 * cstep + 1});
+      cfree = now + cost.chain;
+      evs.push_back({cfree + cost.hop, 0, 0, 0, 2 * cstep + 2});
+      plan.sim_chain.push_back(now);
+      ++cstep;
+    }
+    bool front_busy = false;
+    std::vector<int> idle;
+    for (int p = 0; p < P; ++p) {
+      Worker& w = wk[p];
+      if (w.free > now) {
+        front_busy = front_busy || w.front;
+        continue;
+      }
+      if (w.front && w.held < 0 && fnext < front.size()) w.held = (int)fnext++;
+      if (w.held >= 0) {
+        front_busy = true;
+        const FTask& f = front[w.held];
+        if (!front_ready(f, now)) continue;
+        // S part, then the diagonal block, then the columns as their L blocks become visible (estimated)
+        double tcur = now + cost.fr_s;
+        evs.push_back({tcur + cost.hop, 1, f.i, 0, f.k + 1});
+        int cols[3];
+        const int nc = front_cols(f.k, nblk, cols);
+        for (int q = 0; q < nc; ++q)
+          if (cols[q] == f.i) {
+            tcur += cost.fr_u;
+            evs.push_back({tcur + cost.hop, 2, f.i, f.i, f.k + 1});
+          }
+        for (int q = 0; q < nc; ++q) {
+          const int j = cols[q];
+          if (j >= f.i) continue;
+          const double lvis = j == f.k + 1 ? chainT[2 * f.k + 3] : now + cost.fr_s + cost.hop;  // FR(j, k)'s S part
+          tcur = std::max(tcur, lvis) + cost.fr_u;
+          evs.push_back({tcur + cost.hop, 2, f.i, j, f.k + 1});
+        }
+        w.free = tcur;
+        w.held = -1;
+        continue;
+      }
+      idle.push_back(p);
+    }
+    if (cstep >= nblk && fnext >= front.size() && !front_busy && bulk_left == 0) break;
+    if (idle.empty() || bulk_left == 0) continue;
+    struct Cand { double slack; int q, K; };
+    std::vector<Cand> cands;
+    for (size_t q = 0; q < tiles.size(); ++q) {
+      const BTile& b = tiles[q];
+      const int limit = 2 * b.J - 2;
+      if (b.busy || b.v >= limit) continue;
+      int rel = limit;
+      for (int r : {2 * b.I, 2 * b.I + 1, 2 * b.J, 2 * b.J + 1}) {
+        int v = b.v;
+        while (v < rel && LT(r, v + 1) <= now) ++v;
+        rel = std::min(rel, v);
+      }
+      const int avail = rel - b.v;
+      if (avail <= 0) continue;
+      const double deadline = cfree + (double)(limit - cstep) * cost.chain;
+      const int remaining = limit - b.v;
+      const double rem_t = std::ceil((double)remaining / kMaxChunk) * cost.u128(std::min(remaining, kMaxChunk));
+      const double slack = deadline - now - rem_t;
+      if (avail < kMinChunk && rel < limit && slack > 2 * cost.chain) continue;
+      cands.push_back({slack, (int)q, std::min(avail, kMaxChunk)});
+    }
+    std::sort(cands.begin(), cands.end(), [](const Cand& x, const Cand& y) {
+      return x.slack < y.slack || (x.slack == y.slack && x.q < y.q);
+    });
+    size_t ni = 0;
+    for (const Cand& cd : cands) {
+      if (ni >= idle.size()) break;
+      Worker& w = wk[idle[ni++]];
+      BTile& b = tiles[cd.q];
+      plan.list.push_back(encode(T_U128, b.I, b.J, b.v, b.v + cd.K));
+      const double end = now + cost.u128(cd.K);
+      b.v += cd.K;
+      for (int bi : {2 * b.I, 2 * b.I + 1})
+        for (int bj : {2 * b.J, 2 * b.J + 1})
+          if (bi >= bj) evs.push_back({end + cost.hop, 2, bi, bj, b.v});
+      b.busy = true;
+      evs.push_back({end, 3, cd.q, 0, 0});
+      if (b.v >= 2 * b.J - 2) --bulk_left;
+      w.free = end;
+    }
+  }
+  plan.sim_us = std::max(now, cfree);
+  return plan;
+}
+
+static Plan build_plan(int nblk, int P) {
+  Plan best;
+  best.sim_us = 1e30;
+  for (int div : {8, 6, 4, 3}) {
+    const int F = std::max(1, std::min(nblk, P / div));
+    if (F >= P) continue;
+    Plan p = simulate(nblk, P, F);
+    if (p.sim_us < best.sim_us) best = std::move(p);
+  }
+  return best;
+}
+
+// one plan per (nblk, workers) per handle
+struct Cache {
+  std::map<std::pair<int, int>, std::unique_ptr<Plan>> plans;
+};
+
+}  // namespace dag
+
+size_t potrf_dag_sync_bytes(int npad, int batch) { return (size_t)dag::sync_words(npad / NB) * 4 * batch; }
+
+void potrf_dag_release(Context* c) {
+  auto* cache = reinterpret_cast<dag::Cache*>(c->dag_cache);
+  if (cache) {
+    for (auto& kv : cache->plans)
+      if (kv.second->dev) (void)hipFree(kv.second->dev);
+    delete cache;
+  }
+  c->dag_cache = nullptr;
+  if (c->dag_sync) (void)hipFree(c->dag_sync);
+  c->dag_sync = nullptr;
+  c->dag_sync_bytes = 0;
+}
+
+// Workgroups per problem: one per CU, split evenly over the batch; 0 = the DAG schedule does not apply.
+int potrf_dag_workers(Context* c, int npad, int batch) {
+  const int nblk = npad / NB;
+  if (nblk < 2 || nblk > 64) return 0;
+  if (c->cu_count <= 0) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    c->cu_count = cus;
+  }
+  const int per = c->cu_count / batch;
+  return per >= 8 ? per : 0;
+}
+
+hipError_t launch_potrf_dag(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info,
+                            const Batch& bt, double* W, int64_t ldw) {
+  const int nblk = npad / NB;
+  const int G = potrf_dag_workers(c, npad, bt.count);
+  if (!G) return hipErrorInvalidValue;
+  auto* cache = reinterpret_cast<dag::Cache*>(c->dag_cache);
+  if (!cache) {
+    cache = new dag::Cache();
+    c->dag_cache = cache;
+  }
+  auto key = std::make_pair(nblk, G - 1);
+  auto it = cache->plans.find(key);
+  if (it == cache->plans.end()) {
+    std::unique_ptr<dag::Plan> p(new dag::Plan(dag::build_plan(nblk, G - 1)));
+    const size_t bytes = p->list.size() * sizeof(unsigned long long);
+    if (bytes) {
+      hipError_t e = hipMalloc(&p->dev, bytes);
+      if (e != hipSuccess) return e;
+      e = hipMemcpy(p->dev, p->list.data(), bytes, hipMemcpyHostToDevice);
+      if (e != hipSuccess) return e;
+    }
+    it = cache->plans.emplace(key, std::move(p)).first;
+  }
+  const dag::Plan& plan = *it->second;
+  const size_t sbytes = potrf_dag_sync_bytes(npad, bt.count);
+  if (c->dag_sync_bytes < sbytes) {
+    if (c->dag_sync) (void)hipFree(c->dag_sync);
+    c->dag_sync = nullptr;
+    c->dag_sync_bytes = 0;
+    hipError_t e = hipMalloc(&c->dag_sync, sbytes);
+    if (e != hipSuccess) return e;
+    c->dag_sync_bytes = sbytes;
+  }
+  hipError_t e = hipMemsetAsync(c->dag_sync, 0, sbytes, c->stream);
+  if (e != hipSuccess) return e;
+  dag::Args g;
+  g.A = A;
+  g.lda = lda;
+  g.nblk = nblk;
+  g.Dinv = Dinv;
+  g.info = info;
+  g.W = W;
+  g.ldw = ldw;
+  g.sync = reinterpret_cast<int*>(c->dag_sync);
+  g.sa = bt.k;
+  g.sd = bt.dinv;
+  g.sw = bt.w;
+  g.ss = dag::sync_words(nblk);
+  g.tasks = plan.dev;
+  g.ntasks = (int)plan.list.size();
+  g.nfront = plan.nfront;
+  g.front_workers = plan.front_workers;
+  g.spin_limit = c->spin_limit;
+  dag::potrf_dag_kernel<<<dim3(G, bt.count), WG, 0, c->stream>>>(g);
+  return hipGetLastError();
+}
+
+}  // namespace gpx

@@ -40,7 +40,6 @@ namespace {
 
 constexpr int SB = 128;       // rows per hand-off block
 constexpr int LDT = NB + 1;   // LDS row length of the 64x64 diagonal tiles
-constexpr unsigned kSpinLimit = 1u << 22;
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
@@ -50,7 +49,7 @@ typedef __attribute__((address_space(1))) unsigned gu32;
 // Every wave of a consumer sweeps for itself.  The abort word is read only every 64th failed pass (its sc1 load would
 // otherwise double each poll's round trip).  Returns false on timeout / abort.
 template <int NR>
-__device__ __forceinline__ bool sweep_block(gu64* g, unsigned epoch, double* dst, gu32* abort_word) {
+__device__ __forceinline__ bool sweep_block(gu64* g, unsigned epoch, double* dst, gu32* abort_word, unsigned limit) {
   constexpr int PER = 4 * NR;  // granules per lane: SB * NR * 2 / 64
   const int lane = threadIdx.x & 63;
   unsigned long long x[PER];
@@ -62,8 +61,8 @@ __device__ __forceinline__ bool sweep_block(gu64* g, unsigned epoch, double* dst
       ok &= (unsigned)(x[k] >> 32) == epoch;
     }
     if (__all(ok)) break;
-    if ((spins & 63) == 63 &&
-        (spins >= kSpinLimit || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
+    if (spins >= limit ||
+        ((spins & 63) == 63 && __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
       if (lane == 0) __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return false;
     }
@@ -326,7 +325,7 @@ __device__ __forceinline__ void fma_bwd(double (&acc)[4][NR], const TileRegs& R,
 __device__ void potrs_items_1(int n, int npad, const double* __restrict__ L, int64_t ldl,
                               const double* __restrict__ Dinv, const double* __restrict__ Y, int64_t ldy,
                               double const_mean, double* __restrict__ alpha, gu64* gz, gu64* ga, gu32* abort_word,
-                              SolveLds1& s, int& s_abort) {
+                              unsigned limit, SolveLds1& s, int& s_abort) {
   const int t = threadIdx.x, w = t >> 6;
   const int nb = npad / SB;
   const int G = gridDim.x;
@@ -352,7 +351,7 @@ __device__ void potrs_items_1(int n, int npad, const double* __restrict__ L, int
     if (fwd) {
       if (t < SB) s.vs[t] = (r0 + t < n) ? Y[(r0 + t) * ldy] - const_mean : 0.0;
     } else if (w == 0) {
-      if (!sweep_block<1>(gz + r0 * 2, 1u, s.vs, abort_word) && (t & 63) == 0) s_abort = 1;
+      if (!sweep_block<1>(gz + r0 * 2, 1u, s.vs, abort_word, limit) && (t & 63) == 0) s_abort = 1;
     }
     double acc[4][1];
 #pragma unroll
@@ -360,7 +359,7 @@ __device__ void potrs_items_1(int n, int npad, const double* __restrict__ L, int
     // every wave polls the block it needs into its own LDS copy (no workgroup barrier in the loop)
     double* zw = s.zw[w];
     auto consume = [&](const TileRegs& R, int jj) {
-      if (!sweep_block<1>((fwd ? gz : ga) + (int64_t)jblk(jj) * SB * 2, fwd ? 1u : 2u, zw, abort_word) &&
+      if (!sweep_block<1>((fwd ? gz : ga) + (int64_t)jblk(jj) * SB * 2, fwd ? 1u : 2u, zw, abort_word, limit) &&
           (t & 63) == 0)
         s_abort = 1;
       GPX_POTRS_STAMP(1);
@@ -471,8 +470,8 @@ __device__ void potrs_items_1(int n, int npad, const double* __restrict__ L, int
 template <int NR>
 __device__ void potrs_items(int n, int npad, const double* __restrict__ L, int64_t ldl, const double* __restrict__ Dinv,
                             const double* __restrict__ Y, int64_t ldy, int nrhs, double const_mean,
-                            double* __restrict__ alpha, gu64* gz, gu64* ga, gu32* abort_word, SolveLds<NR>& s,
-                            int& s_abort) {
+                            double* __restrict__ alpha, gu64* gz, gu64* ga, gu32* abort_word, unsigned limit,
+                            SolveLds<NR>& s, int& s_abort) {
   const int t = threadIdx.x, w = t >> 6;
   double* zw = s.zw[w];
   const int nb = npad / SB;
@@ -506,7 +505,7 @@ __device__ void potrs_items(int n, int npad, const double* __restrict__ L, int64
         s.vs[e] = (rr < nrhs && gi < n) ? Y[gi * ldy + rr] - const_mean : 0.0;
       }
     } else if (w == 0) {
-      if (!sweep_block<NR>(gz + r0 * NR * 2, 1u, s.vs, abort_word) && (t & 63) == 0) s_abort = 1;
+      if (!sweep_block<NR>(gz + r0 * NR * 2, 1u, s.vs, abort_word, limit) && (t & 63) == 0) s_abort = 1;
     }
     double acc[4][NR];
 #pragma unroll
@@ -516,7 +515,7 @@ __device__ void potrs_items(int n, int npad, const double* __restrict__ L, int64
     // one register tile (the sweep's 4 NR granules per lane and 4 NR accumulators leave no room for a second one)
     for (int jj = 0; jj < jcount; ++jj) {
       if (jj > 0) load_tile(ta, jj);
-      if (!sweep_block<NR>((fwd ? gz : ga) + (int64_t)jblk(jj) * SB * NR * 2, fwd ? 1u : 2u, zw, abort_word) &&
+      if (!sweep_block<NR>((fwd ? gz : ga) + (int64_t)jblk(jj) * SB * NR * 2, fwd ? 1u : 2u, zw, abort_word, limit) &&
           (t & 63) == 0)
         s_abort = 1;
       if (fwd)
@@ -583,9 +582,9 @@ template <int NR>
 __global__ void __launch_bounds__(WG) potrs_kernel(int n, int npad, const double* __restrict__ L, int64_t ldl,
                                                    const double* __restrict__ Dinv, const double* __restrict__ Y,
                                                    int64_t ldy, int nrhs, double const_mean, double* __restrict__ alpha,
-                                                   const int32_t* __restrict__ info, unsigned long long* granules,
+                                                   int32_t* __restrict__ info, unsigned long long* granules,
                                                    unsigned* abort_ptr, int64_t sl, int64_t sd, int64_t sy, int64_t sa,
-                                                   int64_t sg) {
+                                                   int64_t sg, unsigned limit) {
   const int prob = blockIdx.y;
   L += prob * sl;
   Dinv += prob * sd;
@@ -594,18 +593,22 @@ __global__ void __launch_bounds__(WG) potrs_kernel(int n, int npad, const double
   gu64* gz = (gu64*)(granules + prob * sg);  // forward blocks (epoch 1)
   gu64* ga = gz + (int64_t)npad * NR * 2;     // backward blocks (epoch 2)
   gu32* abort_word = (gu32*)(abort_ptr + prob);
-  if (info && info[prob] != 0) return;  // failed factor: nothing to solve (uniform over the problem's workgroups)
+  if (info && *(volatile int32_t*)(info + prob) != 0) return;  // failed factor: nothing to solve (uniform per problem)
   __shared__ int s_abort;
   if (threadIdx.x == 0) s_abort = 0;
   if constexpr (NR == 1) {
     __shared__ __attribute__((aligned(16))) SolveLds1 s;
     __syncthreads();
-    potrs_items_1(n, npad, L, ldl, Dinv, Y, ldy, const_mean, alpha, gz, ga, abort_word, s, s_abort);
+    potrs_items_1(n, npad, L, ldl, Dinv, Y, ldy, const_mean, alpha, gz, ga, abort_word, limit, s, s_abort);
   } else {
     __shared__ __attribute__((aligned(16))) SolveLds<NR> s;
     __syncthreads();
-    potrs_items<NR>(n, npad, L, ldl, Dinv, Y, ldy, nrhs, const_mean, alpha, gz, ga, abort_word, s, s_abort);
+    potrs_items<NR>(n, npad, L, ldl, Dinv, Y, ldy, nrhs, const_mean, alpha, gz, ga, abort_word, limit, s, s_abort);
   }
+  // a timed-out hand-off: alpha holds NaN; the problem's pivot word reports it (GPX_INFO_TIMEOUT), so a caller that
+  // checks info never mistakes the NaN scores for a result
+  __syncthreads();
+  if (threadIdx.x == 0 && s_abort && info) atomicCAS(info + prob, 0, (int32_t)GPX_INFO_TIMEOUT);
 }
 
 size_t potrs_granule_bytes(int64_t npad, int64_t nrhs) {
@@ -619,7 +622,7 @@ size_t potrs_clear_bytes(int64_t npad, int64_t nrhs, int64_t batch) {
 
 hipError_t launch_potrs(Context* c, int n, int npad, const double* L, int64_t ldl, const double* Dinv,
                         const double* Y, int64_t ldy, int nrhs, double const_mean, double* alpha,
-                        const int32_t* info, void* ws, const Batch& bt, bool ws_cleared) {
+                        int32_t* info, void* ws, const Batch& bt, bool ws_cleared) {
   LaunchTimer tm(c, GPX_TIMER_ALPHA);
   const int nb = npad / SB;
   // granules of every problem, then one abort word per problem; zeroed as ONE block from the workspace start (by the
@@ -631,19 +634,26 @@ hipError_t launch_potrs(Context* c, int n, int npad, const double* L, int64_t ld
     hipError_t e = hipMemsetAsync(ws, 0, potrs_clear_bytes(npad, nrhs, bt.count), c->stream);
     if (e != hipSuccess) return e;
   }
-  // co-resident grid (one 124 KB workgroup per CU at NR = 8): at most 256 workgroups in all
-  int G = 256 / bt.count;
+  // co-resident grid: one workgroup per CU (124 / 135 KB of LDS at NR = 8 / 1), split over the batch
+  if (c->cu_count <= 0) {
+    int dev = 0, cus = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return e;
+    c->cu_count = cus;
+  }
+  int G = c->cu_count / bt.count;
   if (G < 1) G = 1;
   if (G > nb) G = nb;
   const int64_t sg = (int64_t)(gbytes / sizeof(unsigned long long));
   if (nrhs == 1)
     potrs_kernel<1><<<dim3(G, bt.count), WG, 0, c->stream>>>(n, npad, L, ldl, Dinv, Y, ldy, nrhs, const_mean, alpha,
                                                              info, granules, abort_word, bt.k, bt.dinv, bt.y,
-                                                             bt.alpha, sg);
+                                                             bt.alpha, sg, c->spin_limit);
   else
     potrs_kernel<GPX_MAX_RHS><<<dim3(G, bt.count), WG, 0, c->stream>>>(n, npad, L, ldl, Dinv, Y, ldy, nrhs,
                                                                        const_mean, alpha, info, granules, abort_word,
-                                                                       bt.k, bt.dinv, bt.y, bt.alpha, sg);
+                                                                       bt.k, bt.dinv, bt.y, bt.alpha, sg, c->spin_limit);
   return hipGetLastError();
 }
 

@@ -424,21 +424,10 @@ int64_t sweep_chunk_size(int64_t npad, int64_t m) {
   // launch tails and K* / finalize launches until K* outgrows what the Infinity Cache keeps warm for the trmm
   // re-reads).  The byte budget alone sets small-n chunks (tools/small_n_rates.py, 2^22 candidates: a 32768 cap
   // left n = 64 / 256 launch-bound at 3.4e8 / 2.5e8 candidates/s, 1.15e9 / 4.4e8 without it).
-  // GPX_SWEEP_CHUNK_MB / GPX_SWEEP_CHUNK_MAX override budget and cap (experiments).
-  static const int64_t budget_mb = [] {
-    const char* e = getenv("GPX_SWEEP_CHUNK_MB");
-    const long v = e ? atol(e) : 0;
-    return (int64_t)(v > 0 ? v : 1024);
-  }();
-  int64_t cap = budget_mb * ((int64_t)1 << 20) / 8 / npad;
+  int64_t cap = ((int64_t)1 << 30) / 8 / npad;
   cap = (cap / 256) * 256;
   if (cap < 256) cap = 256;
-  static const int64_t max_cands = [] {
-    const char* e = getenv("GPX_SWEEP_CHUNK_MAX");
-    const long v = e ? atol(e) : 0;
-    return (int64_t)(v > 0 ? v : (int64_t)1 << 20);
-  }();
-  if (cap > max_cands) cap = max_cands;
+  if (cap > ((int64_t)1 << 20)) cap = (int64_t)1 << 20;
   int64_t need = ((m + 255) / 256) * 256;
   if (need < 256) need = 256;
   return need < cap ? need : cap;
@@ -458,11 +447,10 @@ size_t sweep_workspace_bytes(int64_t npad, int64_t nrhs, int64_t m) {
 // The fused small-n sweep covers npad <= 256, d <= 16 (1..8 outputs) and the fp64 covariance build; the rest takes
 // the K* + trmm path.  An npad = 384 instance (d <= 8, 226 VGPRs, 2 waves/SIMD) measured slower than the K* + trmm path
 // (2.20e8 vs 2.66e8 candidates/s at n = 384, profiles/r01_small_n_rates.log): 24 row blocks of A operands per k-step
-// from L2 and half the occupancy of the npad = 256 instance.  GPX_SWEEP_FUSED=0 forces the unfused path (A/B
-// measurements, parity tests of both paths).
-bool sweep_fused_ok(const gpx_kernel_params& p, int npad, int nrhs) {
-  const char* e = getenv("GPX_SWEEP_FUSED");  // read per chunk: tests flip it inside one process
-  return !(e && e[0] == '0') && (npad == 128 || npad == 256) && p.d <= 16 && !p.cov_fp32;
+// from L2 and half the occupancy of the npad = 256 instance.  The handle option GPX_OPT_SWEEP_FUSED = 0 forces the
+// unfused path (A/B measurements, parity tests of both paths).
+bool sweep_fused_ok(const Context* c, const gpx_kernel_params& p, int npad, int nrhs) {
+  return c->sweep_fused && (npad == 128 || npad == 256) && p.d <= 16 && !p.cov_fp32;
 }
 
 hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
@@ -474,7 +462,7 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
   const int64_t C = b.chunk;
   int nJB = npad / NB, nI = npad / TT;
   const int ncb = (int)((m_chunk + WG - 1) / WG);  // 256-candidate blocks actually used in this chunk
-  if (sweep_fused_ok(p, npad, nrhs)) {
+  if (sweep_fused_ok(c, p, npad, nrhs)) {
     LaunchTimer tm(c, GPX_TIMER_TRMM);
     const int nwg = (int)((m_chunk + 63) / 64);
 #define GPX_SMALL_K(NP, D, K)                                                                                       \

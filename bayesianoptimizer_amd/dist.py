@@ -3,9 +3,10 @@
 Independent units — restarts / seeds / outputs (BASELINE configs[3]: 32 x n=4096 over 8 GPUs) or contiguous
 candidate shards of one large sweep — are partitioned in contiguous blocks across ranks; every rank fits
 and sweeps its own units with no data-path collective.  The single exchange is one 16-byte
-(fp64 value, int64 global index) record per rank, all-gathered over RCCL (torch.distributed "nccl") and
-reduced deterministically (max value, then lowest global index) by the engine's argmax_combine kernel.
-RCCL has no MAXLOC op, hence gather + local reduce instead of an all-reduce.
+(fp64 value, int64 global index) record per rank: on an nccl group ONE RCCL all-gather through libgpx's own
+communicator (gpx_allreduce_argmax) followed by the deterministic argmax_combine kernel (max value, then lowest global
+index; RCCL has no MAXLOC op, hence gather + local reduce); on gloo the same packed records and the same reduction order
+on the host.  Reference selection site: optimization/Bayesian.py:105-112 (best restart of optimize_acqf).
 """
 from __future__ import annotations
 
@@ -25,44 +26,65 @@ def shard_range(total: int, rank: int, world: int) -> Tuple[int, int]:
     return start, start + q + (1 if rank < r else 0)
 
 
+def pack_record(val: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """The 16-byte exchange record {fp64 value; int64 global index} as two int64 words, exactly as libgpx's
+    record_pack_kernel writes it (gpx_sweep.hip): word 0 = the value's bit pattern, word 1 = the index."""
+    v = val.reshape(1).to(torch.float64).cpu()
+    i = idx.reshape(1).to(torch.int64).cpu()
+    return torch.cat([v.view(torch.int64), i])
+
+
+def unpack_records(recs: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(values, indices) of a (count, 2) int64 record array."""
+    recs = recs.reshape(-1, 2).contiguous()
+    return recs[:, 0].contiguous().view(torch.float64), recs[:, 1].contiguous()
+
+
 def combine_records_host(vals: torch.Tensor, idx: torch.Tensor) -> Tuple[float, int]:
-    """Host reduction with the same order as the device kernel (used for CPU/gloo paths and tests)."""
-    best_v, best_i = float("-inf"), None
+    """Host reduction in the device kernel's order (argmax_final_kernel, gpx_sweep.hip): start from (-inf, INT64_MAX),
+    NaN counts as -inf, a record wins with a larger value or an equal value and a lower index."""
+    best_v, best_i = float("-inf"), 2 ** 63 - 1
     for v, i in zip(vals.reshape(-1).tolist(), idx.reshape(-1).tolist()):
         if v != v:  # NaN never wins
             v = float("-inf")
-        if best_i is None or v > best_v or (v == best_v and i < best_i):
+        if v > best_v or (v == best_v and i < best_i):
             best_v, best_i = v, i
     return best_v, best_i
 
 
-def exchange_argmax(val: torch.Tensor, idx: torch.Tensor, engine=None, group=None):
-    """All-gather every rank's (value, global index) record and reduce it.
+def _rccl_exchange(engine, group) -> "RCCLArgmaxExchange":
+    """libgpx's communicator for (engine, group), created on first use (collective: every rank of the group calls
+    exchange_argmax together, as the exchange itself requires)."""
+    cache = engine.__dict__.setdefault("_rccl_exchanges", {})
+    key = id(group) if group is not None else None
+    ex = cache.get(key)
+    if ex is None:
+        ex = RCCLArgmaxExchange(engine, group)
+        cache[key] = ex
+    return ex
 
-    On GPU tensors with the nccl backend this is RCCL over xGMI and the reduction runs in the engine's
-    argmax_combine kernel; with gloo (CPU tests) the reduction is the identical host loop.
-    Returns (value, index) as 1-element tensors on val's device.
-    """
+
+def exchange_argmax(val: torch.Tensor, idx: torch.Tensor, engine=None, group=None):
+    """Every rank's (value, global index) record -> the global best, with ONE collective per call.
+
+    nccl group (GPU records): libgpx's RCCL communicator (RCCLArgmaxExchange, gpx_allreduce_argmax): one all-gather
+    of the 16-byte records over xGMI and the deterministic argmax_combine kernel on the engine's stream — the path
+    bench.py --gpus N runs.  gloo group (CPU tests): one all-gather of the same packed records, reduced by the host loop
+    in the kernel's order.  Returns (value, index) as 1-element tensors on val's device."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     val = val.reshape(1).to(torch.float64)
     idx = idx.reshape(1).to(torch.int64)
     if world == 1:
-        gv, gi = val, idx
-    else:
-        gv = torch.empty(world, dtype=torch.float64, device=val.device)
-        gi = torch.empty(world, dtype=torch.int64, device=idx.device)
-        if val.is_cuda:
-            dist.all_gather_into_tensor(gv, val, group=group)
-            dist.all_gather_into_tensor(gi, idx, group=group)
-        else:
-            lv = [torch.empty(1, dtype=torch.float64) for _ in range(world)]
-            li = [torch.empty(1, dtype=torch.int64) for _ in range(world)]
-            dist.all_gather(lv, val, group=group)
-            dist.all_gather(li, idx, group=group)
-            gv, gi = torch.cat(lv), torch.cat(li)
-    if engine is not None and gv.is_cuda:
-        return engine.argmax_combine(gv, gi)
-    v, i = combine_records_host(gv, gi)
+        return val, idx
+    if dist.get_backend(group) == "nccl":
+        if engine is None or not val.is_cuda:
+            raise ValueError("the RCCL record exchange needs device records and the engine that owns the communicator")
+        v, i = val.clone(), idx.clone()
+        _rccl_exchange(engine, group)(v, i)
+        return v, i
+    recs = [torch.empty(2, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(recs, pack_record(val, idx), group=group)
+    v, i = combine_records_host(*unpack_records(torch.stack(recs)))
     return (torch.tensor([v], dtype=torch.float64, device=val.device),
             torch.tensor([i], dtype=torch.int64, device=val.device))
 

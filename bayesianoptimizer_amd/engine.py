@@ -24,8 +24,8 @@ import torch
 
 from . import _capi
 from ._capi import (ACQ_EI, ACQ_LOGEI, ACQ_UCB, ACQ_VARIANCE, KERNEL_MATERN52, KERNEL_RBF,
-                    KERNEL_SCALE_LINEAR_MATERN52, AcqParamsC, GPXError, KernelParamsC,
-                    NotPositiveDefiniteError)
+                    KERNEL_SCALE_LINEAR_MATERN52, AcqParamsC, GPXError, GPXTimeoutError, KernelParamsC,
+                    NotPositiveDefiniteError, info_error)
 
 KERNEL_KINDS = {"rbf": KERNEL_RBF, "matern52": KERNEL_MATERN52,
                 "scale_linear_matern52": KERNEL_SCALE_LINEAR_MATERN52}
@@ -36,31 +36,6 @@ def botorch_default_lengthscale(d: int) -> float:
     """Mode of BoTorch's dimension-scaled LogNormal(sqrt2 + log(d)/2, sqrt3) lengthscale prior [upstream]
     (the prior of the SingleTaskGP default covariance reached from optimization/Bayesian.py:91)."""
     return math.exp(math.sqrt(2.0) + 0.5 * math.log(d) - 3.0)
-
-
-class _FactorBuffer:
-    """fp64 device memory from gpx_device_alloc (include/gpx.h), exposed to torch through __cuda_array_interface__:
-    ``torch.as_tensor`` keeps this object alive for as long as any view of the memory lives, and the object keeps its
-    engine (so the handle outlives the allocation).  GPX_ALLOC_UNCACHED keeps the factored matrix's lines out of the
-    XCD L2s' dirty set, which shortens every kernel boundary of the multi-launch Cholesky."""
-
-    def __init__(self, engine: "GPEngine", shape, flags: int):
-        self.engine = engine
-        self.ptr = None
-        nbytes = 8 * math.prod(shape)
-        p = ctypes.c_void_p()
-        _capi.check(engine.lib.gpx_device_alloc(engine.handle, nbytes, flags, ctypes.byref(p)), engine.handle)
-        self.ptr = p.value
-        self.__cuda_array_interface__ = {"shape": tuple(int(v) for v in shape), "typestr": "<f8",
-                                         "data": (self.ptr, False), "strides": None, "version": 2}
-
-    def __del__(self):
-        try:
-            if self.ptr and self.engine.handle is not None:
-                self.engine.lib.gpx_device_free(self.engine.handle, ctypes.c_void_p(self.ptr))
-        except Exception:
-            pass
-        self.ptr = None
 
 
 @dataclass
@@ -149,9 +124,18 @@ class GPState:
         return self.X.shape[1]
 
     def pivot_failure(self) -> int:
-        """0-based failing pivot, or -1 (synchronises)."""
+        """0-based failing pivot, or -1 (synchronises).  A factorisation or triangular solve whose in-launch hand-off
+        timed out (info = GPX_INFO_TIMEOUT) raises GPXTimeoutError: it is not a pivot, and no jitter cures it."""
         v = int(self.info.item())
+        if v < 0:
+            raise info_error(v)
         return v - 1 if v else -1
+
+    def check(self, what: str = "") -> None:
+        """Raise NotPositiveDefiniteError / GPXTimeoutError for a failed update (synchronises)."""
+        err = info_error(int(self.info.item()), what)
+        if err is not None:
+            raise err
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -217,22 +201,15 @@ class GPEngine:
         return ((n + _capi.GPX_TILE - 1) // _capi.GPX_TILE) * _capi.GPX_TILE
 
     # -- fit --------------------------------------------------------------------------------------
-    def factor_buffer(self, shape) -> torch.Tensor:
-        """A fp64 device tensor for a matrix the Cholesky factors in place: an ordinary torch allocation, or with
-        GPX_UNCACHED_FACTOR=1 (experiment only) a zero-copy view of uncached memory (GPX_ALLOC_UNCACHED).  Uncached
-        factors shorten the Cholesky's launch gaps (update 1.83 -> 1.76 ms at n = 4096) but a batched inverse-path fit
-        then differed from its single fit in the last bits on some boxes (tests/test_gpu_parity.py::
-        test_fit_batched_matches_single_fits_and_oracle[300-3-1-True], every run on one box, never with cached memory):
-        off until the ordering of uncached stores across kernel boundaries is understood."""
-        if not hasattr(self, "_uncached_factor"):
-            import os
-            self._uncached_factor = os.environ.get("GPX_UNCACHED_FACTOR", "0") == "1"
-        if not self._uncached_factor or math.prod(shape) == 0:
-            return torch.empty(tuple(shape), dtype=torch.float64, device=self.device)
-        t = torch.as_tensor(_FactorBuffer(self, shape, _capi.GPX_ALLOC_UNCACHED), device=self.device)
-        if t.dtype != torch.float64 or tuple(t.shape) != tuple(shape) or not t.is_cuda:
-            raise GPXError(_capi.GPX_HIP_ERROR, "factor buffer: unexpected tensor from __cuda_array_interface__")
-        return t
+    def set_option(self, name: str, value: int) -> None:
+        """Per-handle tuning / diagnostic option (include/gpx.h GPX_OPT_*: potrf_schedule, spin_limit, sweep_fused,
+        gram_split, potrf_lazy, potrf_mode)."""
+        self._check(self.lib.gpx_set_option(self.handle, _capi.OPTIONS[name], int(value)))
+
+    def get_option(self, name: str) -> int:
+        v = ctypes.c_int64()
+        self._check(self.lib.gpx_get_option(self.handle, _capi.OPTIONS[name], ctypes.byref(v)))
+        return int(v.value)
 
     def alloc_state(self, X: torch.Tensor, nrhs: int, params: KernelParams, capacity: int = 0) -> GPState:
         """Device buffers of one GP; ``capacity`` (training points) reserves room for later ``append`` calls."""
@@ -240,7 +217,7 @@ class GPEngine:
         npad = self.padded_n(n)
         cap = max(npad, self.padded_n(capacity)) if capacity else npad
         dev = self.device
-        Lbuf = self.factor_buffer((cap, cap))
+        Lbuf = torch.empty((cap, cap), dtype=torch.float64, device=dev)
         Wbuf = torch.empty((cap, cap), dtype=torch.float64, device=dev)
         return GPState(
             X=X,
@@ -291,9 +268,7 @@ class GPEngine:
                 _ptr(st.L), st.L.stride(0), _ptr(st.Dinv), _ptr(st.alpha), _ptr(st.info), _ptr(ws), ws.numel()))
         st.W_ready = inverse
         if check:
-            piv = st.pivot_failure()
-            if piv >= 0:
-                raise NotPositiveDefiniteError(piv)
+            st.check()
         return st
 
     def inverse(self, state: GPState) -> GPState:
@@ -399,9 +374,7 @@ class GPEngine:
         state.X, state.L, state.W, state.alpha = X, Lfull, Wfull, alpha
         state.n, state.npad, state._batch = n_new, npad, None
         if check:
-            piv = state.pivot_failure()
-            if piv >= 0:
-                raise NotPositiveDefiniteError(piv)
+            state.check()
         return state
 
     def fit_batched(self, X, Y, params: KernelParams, check: bool = True,
@@ -434,7 +407,7 @@ class GPEngine:
             Lb, Wb, Db, Ab, Ib = out[0]._batch
         else:
             dev = self.device
-            Lb = self.factor_buffer((B, npad, npad))
+            Lb = torch.empty((B, npad, npad), dtype=torch.float64, device=dev)
             Wb = torch.empty((B, npad, npad), dtype=torch.float64, device=dev)
             Db = torch.empty((B, 2 * nblk, 64, 64), dtype=torch.float64, device=dev)
             Ab = torch.empty((B, npad, nrhs), dtype=torch.float64, device=dev)
@@ -462,9 +435,9 @@ class GPEngine:
         if check:
             bad = Ib.cpu().numpy()
             for b in range(B):
-                if bad[b]:
-                    raise NotPositiveDefiniteError(int(bad[b]) - 1, f"problem {b}: not positive definite at pivot "
-                                                                    f"{int(bad[b]) - 1}")
+                err = info_error(int(bad[b]), f"problem {b}")
+                if err is not None:
+                    raise err
         return states
 
     # individual stages (tests and benchmarks)
@@ -636,7 +609,9 @@ class GPEngine:
         # trip per evaluation instead of two; a gradient computed on a failed factor is discarded).
         piv = -1
         for jit in jitters:
-            state = self.fit(X, y, params.replace(jitter=params.jitter + jit), check=False, out=state)
+            # inverse=True: the gradient needs W = L^{-T}; the fused fit forms it from potrf's diagonal inverses and takes
+            # alpha from it (no triangular solve whose alpha the gradient would not use)
+            state = self.fit(X, y, params.replace(jitter=params.jitter + jit), check=False, out=state, inverse=True)
             out = self.mll_grad(state, y)
             v = out.cpu().numpy()
             piv = state.pivot_failure()
@@ -683,9 +658,9 @@ class GPEngine:
             ws.numel()))
         bad = info.cpu().numpy()
         for t in range(T):
-            if bad[t]:
-                raise NotPositiveDefiniteError(int(bad[t]) - 1, f"task {t}: K_ZZ not positive definite at pivot "
-                                                                f"{int(bad[t]) - 1}")
+            err = info_error(int(bad[t]), f"task {t}: K_ZZ")
+            if err is not None:
+                raise err
         return {"Z": Z, "W": W, "W2": W2, "alpha": alpha, "params": list(params), "M": M}
 
     def svgp_predict(self, prep: dict, Xs, min_var: float = 1e-10, want=("mean", "var", "score")):

@@ -38,7 +38,7 @@ class ExactGP:
 
     def __init__(self, train_X, train_Y, params: Optional[KernelParams] = None,
                  outcome_transform: Optional[Standardize] = None, engine=None,
-                 jitter_schedule: Sequence[float] = (0.0, 1e-4, 1e-2)):
+                 jitter_schedule: Sequence[float] = (0.0, 1e-4, 1e-2), capacity: int = 0):
         self.engine = engine if engine is not None else GPEngine()
         dev = getattr(self.engine, "device", None)
         X = torch.as_tensor(train_X, dtype=torch.float64)
@@ -52,6 +52,7 @@ class ExactGP:
         self.params = params or KernelParams("rbf", botorch_default_lengthscale(d), noise=1e-4)
         self.outcome_transform = outcome_transform
         self.jitter_schedule = tuple(jitter_schedule)
+        self.capacity = int(capacity)  # training points the factor's buffers reserve room for (later appends)
         self.state: Optional[GPState] = None
         self.jitter_used = None
         self.mll_result = None
@@ -71,7 +72,10 @@ class ExactGP:
         last = None
         for jit in self.jitter_schedule:
             try:
-                self.state = self.engine.fit(self.train_X, Y, self.params.replace(jitter=jit))
+                if self.capacity > self.train_X.shape[0]:
+                    self.state = self.engine.fit(self.train_X, Y, self.params.replace(jitter=jit), capacity=self.capacity)
+                else:
+                    self.state = self.engine.fit(self.train_X, Y, self.params.replace(jitter=jit))
                 self.jitter_used = jit
                 return self
             except NotPositiveDefiniteError as e:  # reference: retry with larger cholesky_jitter

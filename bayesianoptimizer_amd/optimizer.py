@@ -70,6 +70,15 @@ class GPConfig:
     # with fixed hyperparameters: freeze the input standardisation at the first fit and fold each round's new rows in
     # with the O(n^2 q) bordered update (gpx_append_f64) instead of refitting (Bayesian7.py:639 refits every round)
     incremental_updates: bool = True
+    # Above svgp_threshold training points (where the reference switches to SVGP: optimization/Bayesian6.py:589-596,
+    # scripts/run_optimization.py:40) the drop-in keeps the EXACT posterior over all points but stops paying O(n^3) per
+    # round: hyperparameters are fitted by marginal likelihood on a random subsample of svgp_threshold points and then
+    # held, and each round's new rows are folded in by the bordered update (O(n^2 q)).  The factor is rebuilt (and the
+    # hyperparameters refitted on a fresh subsample) whenever n has grown by this factor since the last rebuild.
+    large_n_refit_growth: float = 2.0
+    # device memory the exact factor may take (L and W = L^{-T}: 2 n^2 doubles at capacity), as a fraction of the free
+    # device memory at the rebuild; beyond it the run stops with a clear error instead of an allocator failure
+    large_n_memory_fraction: float = 0.85
     # acquisition="qlogei": optimize_acqf settings of optimization/Bayesian.py:100-112
     mc_samples: int = 512
     num_restarts: int = 10
@@ -146,7 +155,7 @@ class BayesianOptimizer:
         n_batches: int,
         batch_size: int,
         num_outputs: int = 8,
-        svgp_threshold: int = 100,   # accepted for compatibility: the exact GP serves every size
+        svgp_threshold: int = 3000,  # run_optimization.py:40's value; the large-n policy of GPConfig above it
         resume: bool = False,
         target_total: Optional[int] = None,
         device: Optional[torch.device] = None,
@@ -191,6 +200,7 @@ class BayesianOptimizer:
             if held_out is not None:
                 self.test_X, self.test_Y_raw = self._tensor(self._to_unit(held_out[0])), self._tensor(held_out[1])
         self.gp_model: Optional[ExactGP] = None
+        self._large_n_base: Optional[int] = None  # n at the last large-n rebuild
         self.x_tf: Optional[LogInputStandardizer] = None
         self.y_tf: Optional[LogOutputStandardizer] = None
         self.iteration_counter = 0
@@ -241,22 +251,28 @@ class BayesianOptimizer:
                             linear_variance=c.linear_variance)
 
     def fit_gp_model(self):
-        """Log-standardise (Bayesian7.py:363-385) and build the exact posterior for all outputs on the engine: a fresh
-        fit (hyperparameters by marginal likelihood, or fixed), or — fixed hyperparameters, incremental mode — the
-        previous round's factor extended by the rows observed since."""
+        """Log-standardise (Bayesian7.py:363-385) and build the exact posterior for all outputs on the engine.
+
+        n <= svgp_threshold: a fresh fit each round (hyperparameters by marginal likelihood, or fixed), or - fixed
+        hyperparameters, incremental mode - the previous round's factor extended by the rows observed since.
+        n > svgp_threshold (the reference's SVGP switch, Bayesian6.py:589): the large-n policy (GPConfig)."""
         n = self.train_X.shape[0]
         if n < 1:
             raise RuntimeError("fit_gp_model needs at least one observation")
         cfg = self.config
-        grow = (not cfg.fit_hyperparameters and cfg.incremental_updates and self.gp_model is not None
-                and self.x_tf is not None and self.gp_model.train_X.shape[0] < n)
         self.y_tf = LogOutputStandardizer().fit(self.train_Y_raw)
         Ys = self.y_tf(self.train_Y_raw)
+        if n > self.svgp_threshold:
+            return self._fit_large_n(n, Ys)
+        self._large_n_base = None
+        grow = (not cfg.fit_hyperparameters and cfg.incremental_updates and self.gp_model is not None
+                and self.x_tf is not None and self.gp_model.train_X.shape[0] < n)
         if grow:
             n_old = self.gp_model.train_X.shape[0]
             self.gp_model.train_Y = Ys[:n_old]  # re-standardised targets; alpha is recomputed from all of them
             self.gp_model.append_observations(self.x_tf(self.train_X[n_old:]), Ys[n_old:])
             return self.gp_model
+        self.gp_model = None  # the previous round's factor is released before the next one is allocated
         self.x_tf = LogInputStandardizer(self._bounds_t()).fit(self.train_X)
         self.gp_model = ExactGP(self.x_tf(self.train_X), Ys, self._kernel_params(), engine=self.engine,
                                 jitter_schedule=(0.0, cfg.jitter_val, 1e-2))
@@ -264,6 +280,54 @@ class BayesianOptimizer:
             self.gp_model.fit_hyperparameters(cfg.prior_set, options=cfg.mll_options)
         else:
             self.gp_model.fit()
+        return self.gp_model
+
+    def exact_gp_bytes(self, n: int) -> int:
+        """Device bytes of the exact posterior at n training points: L and W = L^{-T} (2 padded n^2 doubles; the
+        posterior sweep needs W) plus the diagonal-block inverses.  n = 100,000 (main.py:13's --evals): 160 GB, inside
+        one MI355X's 288 GB; the sweep's K* chunk (<= 1 GiB) and the small vectors come on top."""
+        npad = -(-int(n) // _capi.GPX_TILE) * _capi.GPX_TILE
+        return 2 * npad * npad * 8 + 2 * npad * 64 * 8
+
+    def _fit_large_n(self, n: int, Ys: torch.Tensor):
+        """n > svgp_threshold: exact posterior over all n points with hyperparameters from a subsample fit, new rows
+        folded in by the bordered update between rebuilds (GPConfig.large_n_refit_growth)."""
+        cfg = self.config
+        gp = self.gp_model
+        rebuild = (gp is None or self._large_n_base is None or self.x_tf is None
+                   or n >= cfg.large_n_refit_growth * self._large_n_base or gp.train_X.shape[0] > n)
+        if not rebuild:
+            n_old = gp.train_X.shape[0]
+            if n_old < n:
+                gp.train_Y = Ys[:n_old]
+                gp.append_observations(self.x_tf(self.train_X[n_old:]), Ys[n_old:])
+            return gp
+        params = gp.params if gp is not None else self._kernel_params()
+        self.gp_model = gp = None  # release the previous factor (2 n^2 doubles) before the rebuild allocates
+        # room for the rows still to come, within the device memory budget
+        cap = n if self.target_total is None else max(n, min(int(self.target_total), int(cfg.large_n_refit_growth * n)))
+        if torch.cuda.is_available() and getattr(self.gp_device, "type", "cpu") == "cuda":
+            free = torch.cuda.mem_get_info(self.gp_device)[0]
+            budget = cfg.large_n_memory_fraction * free
+            while cap > n and self.exact_gp_bytes(cap) > budget:
+                cap = max(n, int(0.9 * cap))
+            if self.exact_gp_bytes(cap) > budget:
+                raise MemoryError(f"exact GP at n={n} needs {self.exact_gp_bytes(n) / 1e9:.1f} GB of device memory, "
+                                  f"{budget / 1e9:.1f} GB available (GPConfig.large_n_memory_fraction)")
+        self.x_tf = LogInputStandardizer(self._bounds_t()).fit(self.train_X)
+        Xs = self.x_tf(self.train_X)
+        jit = (0.0, cfg.jitter_val, 1e-2)
+        if cfg.fit_hyperparameters:
+            m = int(self.svgp_threshold)
+            sub = np.sort(self._rng.choice(n, size=m, replace=False))
+            sub_t = torch.as_tensor(sub, device=Xs.device)
+            sub_gp = ExactGP(Xs[sub_t], Ys[sub_t], params, engine=self.engine, jitter_schedule=jit)
+            sub_gp.fit_hyperparameters(cfg.prior_set, options=cfg.mll_options)
+            params = sub_gp.params
+            del sub_gp
+            print(f"[gpx] n={n} > svgp_threshold={self.svgp_threshold}: hyperparameters from a {m}-point subsample")
+        self.gp_model = ExactGP(Xs, Ys, params, engine=self.engine, jitter_schedule=jit, capacity=cap).fit()
+        self._large_n_base = n
         return self.gp_model
 
     def predict(self, x_orig_numpy: np.ndarray, return_var: bool = False):

@@ -16,9 +16,11 @@
  *  - Calls are asynchronous on the handle's stream (gpx_set_stream) and never allocate device memory;
  *    scratch comes from the caller's workspace (size from the *_workspace_size queries).
  *  - Errors: return a gpx_status; gpx_last_error(h) gives a message.  NOT_PD is reported through a device
- *    int32 `info` (0 = OK, else failing pivot + 1, LAPACK potrf convention) so the fit stays asynchronous;
+ *    int32 `info` (0 = OK, > 0 failing pivot + 1, LAPACK potrf convention) so the fit stays asynchronous;
  *    gpx_fit_f64_sync reads it back and returns GPX_NOT_PD, like the reference's jitter-retry path
- *    (optimization/Bayesian6.py:481-488) expects an exception.
+ *    (optimization/Bayesian6.py:481-488) expects an exception.  info = GPX_INFO_TIMEOUT (negative) means an
+ *    in-launch hand-off of the factorisation or of the triangular solve gave up after its bounded spin
+ *    (gpx_fit_f64_sync: GPX_TIMEOUT); the factor / alpha are then invalid.
  */
 #ifndef GPX_H
 #define GPX_H
@@ -46,8 +48,10 @@ enum {
   GPX_NOT_PD = 1,
   GPX_INVALID_ARG = 2,
   GPX_HIP_ERROR = 3,
-  GPX_RCCL_ERROR = 4
+  GPX_RCCL_ERROR = 4,
+  GPX_TIMEOUT = 5 /* a persistent launch's hand-off timed out (device info = GPX_INFO_TIMEOUT) */
 };
+#define GPX_INFO_TIMEOUT ((int32_t)0x80000000)
 
 /* Covariance modules used by the reference.
  * RBF: BoTorch SingleTaskGP default (optimization/Bayesian.py:91, Bayesian1.py:109) [upstream]
@@ -125,16 +129,28 @@ int64_t gpx_padded_n(int64_t n);
 size_t gpx_kernel_params_size(void);
 size_t gpx_acq_params_size(void);
 
-/* Device memory for the factored matrix (no reference counterpart: an allocation policy of this library).  flags:
- * GPX_ALLOC_DEFAULT (hipMalloc) or GPX_ALLOC_UNCACHED (hipExtMallocWithFlags(hipDeviceMallocUncached): lines of the
- * buffer are not kept dirty in the XCD L2s, so the kernel-boundary write-back between the Cholesky's dependent launches
- * has nothing to flush: launch gap 3.3 -> 1.8 us, potrf n = 4096 1.75 -> 1.67 ms).  EXPERIMENTAL: a batched fit
- * on an uncached factor differed from its single fit in the last bits on one box, so the Python engine does not use
- * it by default.  Freed with gpx_device_free on the same handle's device. */
-#define GPX_ALLOC_DEFAULT 0
-#define GPX_ALLOC_UNCACHED 1
-gpx_status gpx_device_alloc(gpx_handle h, size_t bytes, int32_t flags, void** out);
-gpx_status gpx_device_free(gpx_handle h, void* ptr);
+/* Per-handle options (tuning and diagnostics; every default is the measured best).  gpx_create reads the environment
+ * variable GPX_OPTIONS once ("name=value,name=value", names as below in lower case without the prefix, e.g.
+ * "potrf_schedule=1,sweep_fused=0"); nothing else in the library reads the environment.
+ *  GPX_OPT_POTRF_SCHEDULE  0 by size (default: one persistent dataflow launch for padded n <= 4096, one launch per
+ *                          block column above), 1 multi-launch everywhere, 2 dataflow wherever it applies
+ *  GPX_OPT_SPIN_LIMIT      polls before an in-launch hand-off (Cholesky dataflow, triangular solve) gives up and
+ *                          reports GPX_INFO_TIMEOUT (default 4194304; 0 = give up at the first unmet poll: tests)
+ *  GPX_OPT_SWEEP_FUSED     1 (default) the fused small-n sweep where it applies (padded n <= 256), 0 the K* + trmm path
+ *  GPX_OPT_GRAM_SPLIT      0 by size (default), else 1, 2 or 4 workgroups per 64x64 Gram tile
+ *  GPX_OPT_POTRF_LAZY      multi-launch schedule: 0 by size (default), else flush the trailing update every g columns
+ *  GPX_OPT_POTRF_MODE      multi-launch schedule: -1 by size (default), 0 eager panels, 1 lookahead panels */
+enum {
+  GPX_OPT_POTRF_SCHEDULE = 0,
+  GPX_OPT_SPIN_LIMIT = 1,
+  GPX_OPT_SWEEP_FUSED = 2,
+  GPX_OPT_GRAM_SPLIT = 3,
+  GPX_OPT_POTRF_LAZY = 4,
+  GPX_OPT_POTRF_MODE = 5,
+  GPX_OPT_COUNT = 6
+};
+gpx_status gpx_set_option(gpx_handle h, int32_t option, int64_t value);
+gpx_status gpx_get_option(gpx_handle h, int32_t option, int64_t* value_host);
 
 /* ---- fit = posterior update ----------------------------------------------- */
 /* Gram K(X,X)+(noise+jitter)I into the lower triangle of the padded K (replaces the covar_module(X) +
@@ -184,11 +200,12 @@ gpx_status gpx_fit_f64_sync(gpx_handle h, const gpx_kernel_params* p, int64_t n,
 /* alpha = K^{-1} (Y - const_mean) from the factor alone (LAPACK potrs): forward L z = Y - m, backward L^T alpha = z,
  * with L and Dinv as gpx_potrf_f64 left them (no W needed).  Y: n x nrhs (leading dim ldy), alpha: contiguous
  * padded_n x nrhs (rows >= n are 0).  info (device, nullable): the factor's pivot word — a failed factor (non-zero)
- * leaves alpha untouched.  One launch; its workgroups hand 128-row blocks of z / alpha to each other inside it
- * (deterministic: fixed accumulation order).  Replaces the ExactGP mean_cache [upstream]. */
+ * leaves alpha untouched; a solve whose in-launch hand-off times out writes GPX_INFO_TIMEOUT into it (and NaN into
+ * alpha).  One launch; its workgroups hand 128-row blocks of z / alpha to each other inside it (deterministic: fixed
+ * accumulation order).  Replaces the ExactGP mean_cache [upstream]. */
 gpx_status gpx_potrs_workspace_size(int64_t n, int64_t nrhs, size_t* bytes);
 gpx_status gpx_potrs_f64(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv, const double* Y,
-                         int64_t ldy, int64_t nrhs, double const_mean, double* alpha, const int32_t* info, void* ws,
+                         int64_t ldy, int64_t nrhs, double const_mean, double* alpha, int32_t* info, void* ws,
                          size_t ws_bytes);
 
 /* The posterior update as SURVEY §8d defines it — Gram + Cholesky + alpha — WITHOUT the explicit inverse: alpha by

@@ -39,8 +39,9 @@ class OracleEngine:
     def __init__(self):
         self.calls = {"fit": 0, "posterior": 0, "acquire": 0}
 
-    def fit(self, X, Y, params, check=True, out=None):
+    def fit(self, X, Y, params, check=True, out=None, capacity=0):
         self.calls["fit"] += 1
+        self.calls["fit_n"] = self.calls.get("fit_n", []) + [int(np.asarray(X).shape[0])]
         X = torch.as_tensor(X, dtype=torch.float64).cpu().numpy()
         Y = torch.as_tensor(Y, dtype=torch.float64).cpu().numpy()
         if Y.ndim == 1:
@@ -53,6 +54,7 @@ class OracleEngine:
 
     def mll_value_grad(self, X, Y, params, jitters=(0.0, 1e-8, 1e-7, 1e-6), state=None):
         self.calls["mll"] = self.calls.get("mll", 0) + 1
+        self.calls["mll_n"] = self.calls.get("mll_n", set()) | {int(np.asarray(X).shape[0])}
         X = torch.as_tensor(X, dtype=torch.float64).cpu().numpy()
         Y = torch.as_tensor(Y, dtype=torch.float64).cpu().numpy()
         err = None

@@ -45,3 +45,28 @@ def test_dropin_gpu_model_matches_oracle_engine(tmp_path, engine):
     np.testing.assert_allclose(y_gpu, y_cpu, rtol=1e-8, atol=1e-10)
     for s in sims:
         s.cleanup()
+
+
+def test_dropin_crosses_svgp_threshold_on_gpu(tmp_path, engine):
+    """The driver's threshold (scripts/run_optimization.py:40: 3000): below it the GP is refitted by marginal
+    likelihood each round, above it hyperparameters come from a 3000-point subsample, the exact posterior covers every
+    point, and later rounds use the bordered update; the posterior then equals a fresh fit on the same data."""
+    from bayesianoptimizer_amd.models import ExactGP
+    from oracle import gp_oracle as O
+
+    cfg = GPConfig(candidates_pool_size=2048, acq_batch_size=20, fit_hyperparameters=True, prior_set="none",
+                   mll_options={"maxiter": 15})
+    opt = BayesianOptimizer(StubSimulator(), BOUNDS, str(tmp_path), n_initial_points=2990, n_batches=3, batch_size=20,
+                            svgp_threshold=3000, target_total=3050, engine=engine, gp_config=cfg, seed=1)
+    opt.optimize()
+    opt.fit_gp_model()
+    gp = opt.gp_model
+    assert opt.train_X.shape[0] == 3050
+    assert opt._large_n_base == 3010          # the first round above the threshold rebuilt the factor
+    assert gp.state.n == 3050                 # the rows since were folded in by the bordered update
+    ref = ExactGP(gp.train_X, opt.y_tf(opt.train_Y_raw), gp.params, engine=engine).fit()
+    Xq = opt.x_tf(torch.tensor(O.sobol_candidates(512, 5, 3), device=engine.device))
+    a, b = gp.posterior(Xq), ref.posterior(Xq)
+    scale = b.mean.abs().max()
+    assert (a.mean - b.mean).abs().max() <= 1e-9 * scale
+    assert (a.variance - b.variance).abs().max() <= 1e-9 * b.variance.abs().max()

@@ -1,9 +1,7 @@
 """Fused small-n sweep (sweep_small_kernel: npad <= 256, d <= 16, 1..8 outputs, fp64 covariance build; n = 257..384
 cases check the boundary, where both sides take the K* + trmm path): every case is checked against the oracle at the parity tolerances of tests/test_gpu_parity.py, and against the unfused K* + trmm path
-of the same library (GPX_SWEEP_FUSED=0, read per chunk) — the two paths sum in different orders, so they agree to the
+of the same library (handle option sweep_fused = 0, GPX_OPT_SWEEP_FUSED) — the two paths sum in different orders, so they agree to the
 same 1e-9 tolerance, and their argmax agrees exactly or at a reported tie."""
-import os
-
 import numpy as np
 import pytest
 
@@ -15,12 +13,12 @@ ACQS = {"ei": O.ACQ_EI, "logei": O.ACQ_LOGEI, "ucb": O.ACQ_UCB, "variance": O.AC
 
 
 def _run(engine, st, Xs, acq, best_f, fused):
-    os.environ["GPX_SWEEP_FUSED"] = "1" if fused else "0"
+    engine.set_option("sweep_fused", 1 if fused else 0)
     try:
         mu, var = engine.posterior(st, t(Xs))
         bv, bi, sg = engine.acquire(st, t(Xs), acq, best_f=best_f, return_scores=True)
     finally:
-        os.environ.pop("GPX_SWEEP_FUSED", None)
+        engine.set_option("sweep_fused", 1)
     return mu.cpu().numpy(), var.cpu().numpy(), int(bi.item()), sg.cpu().numpy()
 
 
@@ -91,11 +89,11 @@ def test_fused_multi_output_posterior(engine, n, d, nrhs, kind):
     Xs = O.sobol_candidates(3000, d, n)
     out = {}
     for fused in (True, False):
-        os.environ["GPX_SWEEP_FUSED"] = "1" if fused else "0"
+        engine.set_option("sweep_fused", 1 if fused else 0)
         try:
             mu, var = engine.posterior(st, t(Xs))
         finally:
-            os.environ.pop("GPX_SWEEP_FUSED", None)
+            engine.set_option("sweep_fused", 1)
         out[fused] = (mu.cpu().numpy(), var.cpu().numpy())
     mu_r, var_r = O.posterior(ost, Xs)
     kdiag = O.kernel_diag(Xs, op)

@@ -227,3 +227,39 @@ def test_dropin_incremental_updates_match_refit(tmp_path):
     ref = ExactGP(gp.train_X, opt.y_tf(opt.train_Y_raw), gp.params, engine=OracleEngine()).fit()
     Xq = opt.x_tf(torch.tensor(O.sobol_candidates(16, 5, 1)))
     torch.testing.assert_close(gp.posterior(Xq).mean, ref.posterior(Xq).mean, rtol=1e-9, atol=1e-9)
+
+
+def test_dropin_large_n_policy_switches_at_threshold(tmp_path):
+    """Above svgp_threshold (the reference's SVGP switch, optimization/Bayesian6.py:589; run_optimization.py:40) the
+    drop-in keeps the exact posterior over all points but fits hyperparameters on a threshold-sized subsample only and
+    folds later rows in by the bordered update; below it every round refits by marginal likelihood."""
+    cfg = GPConfig(candidates_pool_size=256, acq_batch_size=6, fit_hyperparameters=True, prior_set="none",
+                   mll_options={"maxiter": 8})
+    eng = OracleEngine()
+    opt = BayesianOptimizer(StubSimulator(), BOUNDS, str(tmp_path), n_initial_points=24, n_batches=4, batch_size=6,
+                            svgp_threshold=28, target_total=48, engine=eng, gp_config=cfg, seed=5)
+    opt.optimize()
+    opt.fit_gp_model()
+    n = opt.train_X.shape[0]
+    assert n == 48
+    # marginal-likelihood fits ran at n = 24 (below the threshold) and on the 28-point subsample, never on all points
+    assert eng.calls["mll_n"] <= {24, 28}, eng.calls["mll_n"]
+    assert 28 in eng.calls["mll_n"]
+    assert eng.calls.get("append", 0) >= 2
+    gp = opt.gp_model
+    ref = ExactGP(gp.train_X, opt.y_tf(opt.train_Y_raw), gp.params, engine=OracleEngine()).fit()
+    Xq = opt.x_tf(torch.tensor(O.sobol_candidates(16, 5, 2)))
+    torch.testing.assert_close(gp.posterior(Xq).mean, ref.posterior(Xq).mean, rtol=1e-9, atol=1e-9)
+
+
+def test_dropin_large_n_rebuilds_after_growth(tmp_path):
+    cfg = GPConfig(candidates_pool_size=128, acq_batch_size=8, fit_hyperparameters=False, large_n_refit_growth=1.5)
+    eng = OracleEngine()
+    opt = BayesianOptimizer(StubSimulator(), BOUNDS, str(tmp_path), n_initial_points=20, n_batches=4, batch_size=8,
+                            svgp_threshold=16, target_total=52, engine=eng, gp_config=cfg, seed=6)
+    opt.optimize()
+    # n = 20 (> 16): rebuild; 28, 36 appended; 44 >= 1.5 * 28?  no: base 20 -> rebuild at n >= 30 (n = 36), base 36 ->
+    # the next rebuild would come at 54
+    assert opt._large_n_base == 36
+    assert 20 in eng.calls["fit_n"] and 36 in eng.calls["fit_n"]
+    assert opt.exact_gp_bytes(100_000) == 2 * 100_096 ** 2 * 8 + 2 * 100_096 * 64 * 8
