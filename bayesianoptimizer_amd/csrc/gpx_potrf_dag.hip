@@ -52,7 +52,7 @@ namespace dag {
 constexpr int LD = LD64;              // LDS row length of a 64x64 tile (doubles)
 constexpr int TILE_D = NB * LD;       // doubles per LDS tile
 constexpr int HDR = 16;               // sync words before the per-row counters
-enum { W_CHAIN = 0, W_ABORT = 1, W_TICKET_FRONT = 2, W_TICKET_BULK = 3 };
+enum { W_CHAIN = 0, W_ABORT = 1, W_TICKET = 2 };  // tickets: W_TICKET + list (0 critical, 1 front, 2 bulk)
 enum { T_FR = 1, T_U64 = 2, T_U128 = 3 };
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -88,7 +88,7 @@ struct Sync {
   int nblk;
   __device__ int* chain() const { return w + W_CHAIN; }
   __device__ int* abort_word() const { return w + W_ABORT; }
-  __device__ int* ticket(int which) const { return w + W_TICKET_FRONT + which; }
+  __device__ int* ticket(int which) const { return w + W_TICKET + which; }
   __device__ int* lrow(int i) const { return w + HDR + i; }
   __device__ int* ver(int i, int j) const { return w + HDR + nblk + i * nblk + j; }
 };
@@ -252,7 +252,7 @@ __device__ __forceinline__ void rowblock_out(const d4 (&acc)[4], int w, double* 
 //      final through column c-1 and, once they are, load them into sB / sN (the 64 x 128 strip, one third per wave).
 // Out: sA = L_cc (lower 16-blocks), sX = D_c.  Returns the failing pivot 0..63 or -1, uniform; *pref == 3: prefetched.
 struct ChainShared {
-  int cnt, srow, fail, pref, prefdone;
+  int cnt, srow, fail, pref, prefdone, pub;
 };
 
 __device__ __forceinline__ void prefetch_share(const double* strip, int64_t ld, double* sB, double* sN, int w) {
@@ -279,8 +279,38 @@ __device__ __forceinline__ void prefetch_share(const double* strip, int64_t ld, 
   }
 }
 
-__device__ __forceinline__ int chain_step(const Sync& s, int c, int nblk, double* A, int64_t lda, double* sA,
-                                          double* sB, double* sX, double* sN, ChainShared& sh) {
+// Output of the previous step by waves 1-3 (one third of the rows each): L_pp (its lower 16-blocks, zeros above)
+// and D_p into global memory (sc1), and - for a fit that forms W - W_pp = D_p^T (plain stores: W is not read in the
+// launch) with the strictly lower 64-block of an odd 128-tile zeroed.
+__device__ __forceinline__ void store_prev(const double* sL, const double* sD, double* Lg, int64_t lda, double* Dg,
+                                           double* W, int64_t ldw, int p, int w) {
+  const int lane = threadIdx.x & 63;
+  const rsrc_t rl = rsrc(Lg), rd = rsrc(Dg);
+  const int col = 2 * (lane & 31);
+  for (int row = (w - 1) * 2 + (lane >> 5); row < NB; row += 6) {
+    double a = sL[row * LD + col], b = sL[row * LD + col + 1];
+    if ((col >> 4) > (row >> 4)) a = b = 0.0;
+    st2(rl, (int)(((int64_t)row * lda + col) * 8), a, b);
+    double x = sD[row * LD + col], y = sD[row * LD + col + 1];
+    if ((col >> 4) > (row >> 4)) x = y = 0.0;
+    st2(rd, (int)(((int64_t)row * NB + col) * 8), x, y);
+  }
+  if (W) {
+    double* Wpp = W + (int64_t)p * NB * ldw + (int64_t)p * NB;
+    for (int e = threadIdx.x - 64; e < NB * NB; e += WG - 64) {
+      const int r = e >> 6, cc = e & 63;
+      Wpp[(int64_t)r * ldw + cc] = ((r >> 4) > (cc >> 4)) ? 0.0 : sD[cc * LD + r];
+    }
+    if (p & 1) {
+      double* Z = W + (int64_t)p * NB * ldw + (int64_t)(p - 1) * NB;
+      for (int e = threadIdx.x - 64; e < NB * NB; e += WG - 64) Z[(int64_t)(e >> 6) * ldw + (e & 63)] = 0.0;
+    }
+  }
+}
+
+__device__ __forceinline__ int chain_step(const Sync& s, int c, int nblk, double* A, int64_t lda, double* Dinv,
+                                          double* W, int64_t ldw, double* sA, double* sB, double* sX, double* sN,
+                                          ChainShared& sh) {
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   auto dblk = [&](int q) { return sX + 16 * q * LD + 16 * q; };
   auto tsolve = [&](int i, int q) {
@@ -293,10 +323,14 @@ __device__ __forceinline__ int chain_step(const Sync& s, int c, int nblk, double
     acc = mfma_lds16<true>(acc, sA, 16 * i, 16 * q, sA, 16 * q, 16 * j, 16, -1.0);
     store_block16(sA, 16 * i, 16 * j, acc);
   };
-  auto xitem = [&](int q, int j) {
+  // sum_{k=j}^{q-1} L_qk X_kj (acc layout), and X_qj = -D_qq P: the accumulator register r of P is the B operand of
+  // k-step r (rows 4r + lane/16)
+  auto xpart = [&](int q, int j) {
     d4 acc = {0.0, 0.0, 0.0, 0.0};
     for (int k = j; k < q; ++k) acc = mfma_lds16<false>(acc, sA, 16 * q, 16 * k, sX, 16 * k, 16 * j, 16, 1.0);
-    // X_qj = -D_qq acc: the accumulator register r is the B operand of k-step r (rows 4r + lane/16)
+    return acc;
+  };
+  auto xfinish = [&](int q, int j, const d4& acc) {
     const int m = lane & 15, kk = lane >> 4;
     d4 x = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -304,7 +338,9 @@ __device__ __forceinline__ int chain_step(const Sync& s, int c, int nblk, double
     store_block16(sX, 16 * q, 16 * j, x);
   };
   auto lds_add = [&](int* word) {
-    if (lane == 0) __hip_atomic_fetch_add(word, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    int old = 0;
+    if (lane == 0) old = __hip_atomic_fetch_add(word, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __builtin_amdgcn_readfirstlane(old);
   };
   auto lds_wait = [&](int* word, int want) {
     while (__hip_atomic_load(word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < want) __builtin_amdgcn_s_sleep(1);
@@ -331,9 +367,16 @@ __device__ __forceinline__ int chain_step(const Sync& s, int c, int nblk, double
     sh.fail = -1;
     sh.pref = 0;
     sh.prefdone = 0;
+    sh.pub = 0;
   }
   __syncthreads();
   if (c > 0) {
+    if (w > 0) {
+      // the previous step's L_{c-1,c-1} (in sN) and D_{c-1} (in sX) leave while wave 0 starts this step; the last of
+      // waves 1-3 to drain them publishes chain word 2c (D_{c-1} readable: the stage c-1 tasks of the pool start)
+      store_prev(sN, sX, A + (int64_t)(c - 1) * NB * lda + (int64_t)(c - 1) * NB, lda,
+                 Dinv + (int64_t)(c - 1) * NB * NB, W, ldw, c - 1, w);
+    }
     d4 acc[4];
     rowblock_times_lower_t(acc, sB, sX, w);  // reads only this wave's rows of sB
     rowblock_out(acc, w, A + (int64_t)c * NB * lda + (int64_t)(c - 1) * NB, lda, sB);
@@ -343,9 +386,12 @@ __device__ __forceinline__ int chain_step(const Sync& s, int c, int nblk, double
       d4 u = load_block16(sA, 0, 0);
       u = mfma_lds16<true>(u, sB, 0, 0, sB, 0, 0, NB, -1.0);
       store_block16(sA, 0, 0, u);
-      lds_wait(&sh.srow, 4);  // every wave's S reads of D_{c-1} are done before chol16 overwrites sX
+      lds_wait(&sh.srow, 4);  // every wave's S reads of D_{c-1} (and stores of it) are done before chol16 overwrites sX
       GPX_DAG_STAMP(0, c, 0, 2);
     } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lds_add(&sh.pub) == 2 && lane == 0)
+        __hip_atomic_store(s.chain(), 2 * c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       lds_wait(&sh.srow, 4);
       if (w == 1) syrk3<1, 0, 2, 1, 3, 1>(sA, sB);
       else if (w == 2) syrk3<1, 1, 2, 2, 3, 2>(sA, sB);
@@ -354,6 +400,7 @@ __device__ __forceinline__ int chain_step(const Sync& s, int c, int nblk, double
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // L_{c,c-1} drained before the first barrier (published after it)
   }
   int fail = -1;
+  d4 ptail = {0.0, 0.0, 0.0, 0.0};  // waves 1-3: sum_{k=j}^{2} L_3k X_kj of their block X_3j (j = w - 1), from q = 2
   for (int q = 0; q < 4; ++q) {
     if (w == 0) {
       const int f = chol16<LD>(sA, dblk(q), 16 * q);
@@ -378,8 +425,18 @@ __device__ __forceinline__ int chain_step(const Sync& s, int c, int nblk, double
           if (1 + e % 3 == w) update(i, j, q);
           ++e;
         }
-      for (int j = 0; j < q; ++j)
-        if (1 + j % 3 == w) xitem(q, j);
+      if (q < 3) {
+        for (int j = 0; j < q; ++j)
+          if (1 + j % 3 == w) xfinish(q, j, xpart(q, j));
+      }
+      if (q == 2) {
+        // block row 3 of the inverse up to its last factor: X_3j = -D_33 P_3j with P_3j = sum_{k=j}^{2} L_3k X_kj.
+        // Wave w takes j = w - 1: X_20 / X_21 are this wave's own step-2 items (wave 1 / 2), L_32 is wave 0's
+        // lookahead item (published before the counter above reached 12).
+        ptail = xpart(3, w - 1);
+      } else if (q == 3) {
+        xfinish(3, w - 1, ptail);
+      }
       if (q == 1 || q == 2) try_prefetch();
     }
   }
@@ -461,8 +518,9 @@ struct Args {
   int64_t ldw;
   int* sync;
   int64_t sa, sd, sw, ss;  // per-problem strides (A, Dinv, W in doubles; sync in ints)
-  const unsigned long long* tasks;  // front tasks [0, nfront), bulk tasks [nfront, ntasks)
-  int ntasks, nfront, front_workers;
+  const unsigned long long* tasks;  // critical [0, lend[0]), front [lend[0], lend[1]), bulk [lend[1], lend[2])
+  int lend[3];
+  int wend[2];  // workers: blockIdx.x in [1, wend[0]) critical, [wend[0], wend[1]) front, the rest bulk
   unsigned spin_limit;
 };
 
@@ -481,7 +539,7 @@ __device__ void chain_role(const Args& g, double* A, double* Dinv, double* W, in
   __syncthreads();
   for (int c = 0; c < nblk; ++c) {
     GPX_DAG_STAMP(0, c, 0, 0);
-    const int f = chain_step(s, c, nblk, A, lda, sA, sB, sX, sN, sh);
+    const int f = chain_step(s, c, nblk, A, lda, Dinv, W, g.ldw, sA, sB, sX, sN, sh);
     if (f >= 0) {
       if (t == 0) {
         atomicCAS(info, 0, c * NB + f + 1);
@@ -489,35 +547,37 @@ __device__ void chain_role(const Args& g, double* A, double* Dinv, double* W, in
       }
       break;
     }
-    tile_out<true>(sA, blk(c, c), lda);
-    tile_out<true>(sX, Dinv + (int64_t)c * NB * NB, NB);
-    if (W) {  // what potrf_dinv does for a fit with an inverse: W_cc = D_c^T, the lower block of an odd 128-tile zeroed
-      double* Wcc = W + (int64_t)c * NB * g.ldw + (int64_t)c * NB;
-      for (int e = t; e < NB * NB; e += WG) {
-        const int r = e >> 6, cc = e & 63;
-        Wcc[(int64_t)r * g.ldw + cc] = ((r >> 4) > (cc >> 4)) ? 0.0 : sX[cc * LD + r];
+    if (c + 1 == nblk) {  // the last factor and inverse (earlier ones leave during the next step)
+      tile_out<true>(sA, blk(c, c), lda);
+      tile_out<true>(sX, Dinv + (int64_t)c * NB * NB, NB);
+      if (W) {
+        double* Wcc = W + (int64_t)c * NB * g.ldw + (int64_t)c * NB;
+        for (int e = t; e < NB * NB; e += WG) {
+          const int r = e >> 6, cc = e & 63;
+          Wcc[(int64_t)r * g.ldw + cc] = ((r >> 4) > (cc >> 4)) ? 0.0 : sX[cc * LD + r];
+        }
+        if (c & 1) {
+          double* Z = W + (int64_t)c * NB * g.ldw + (int64_t)(c - 1) * NB;
+          for (int e = t; e < NB * NB; e += WG) Z[(int64_t)(e >> 6) * g.ldw + (e & 63)] = 0.0;
+        }
       }
-      if (c & 1) {
-        double* Z = W + (int64_t)c * NB * g.ldw + (int64_t)(c - 1) * NB;
-        for (int e = t; e < NB * NB; e += WG) Z[(int64_t)(e >> 6) * g.ldw + (e & 63)] = 0.0;
-      }
+      wg_publish(t == 0 ? s.chain() : nullptr, 2 * c + 2);
+      GPX_DAG_STAMP(0, c, 0, 8);
+      break;
     }
-    wg_publish(t == 0 ? s.chain() : nullptr, 2 * c + 2);
     GPX_DAG_STAMP(0, c, 0, 8);
-    if (c + 1 < nblk) {
-      if (sh.prefdone < 3) {  // the next tiles were not final during the factorisation: wait, then load them
-        const int lane = t & 63;
-        const int* mine = lane == 0 ? s.ver(c + 1, c) : (lane == 1 ? s.ver(c + 1, c + 1) : nullptr);
-        if (!wg_wait(s, mine, c, g.spin_limit)) break;
-        tile_in(blk(c + 1, c), lda, sB);
-        tile_in(blk(c + 1, c + 1), lda, sN);
-      }
-      __syncthreads();
-      GPX_DAG_STAMP(0, c, 0, 9);
-      double* tmp = sA;
-      sA = sN;
-      sN = tmp;
+    if (sh.prefdone < 3) {  // the next tiles were not final during the factorisation: wait, then load them
+      const int lane = t & 63;
+      const int* mine = lane == 0 ? s.ver(c + 1, c) : (lane == 1 ? s.ver(c + 1, c + 1) : nullptr);
+      if (!wg_wait(s, mine, c, g.spin_limit)) break;
+      tile_in(blk(c + 1, c), lda, sB);
+      tile_in(blk(c + 1, c + 1), lda, sN);
     }
+    __syncthreads();
+    GPX_DAG_STAMP(0, c, 0, 9);
+    double* tmp = sA;  // sA (L_cc, stored during the next step) becomes the next prefetch target
+    sA = sN;
+    sN = tmp;
   }
 }
 
@@ -545,18 +605,9 @@ __device__ bool task_fr(const Args& g, double* A, double* Dinv, const Sync& s, i
   int cols[3];
   const int ncol = front_cols(k, g.nblk, cols);
   {
-    // lane 0: D_k published; lane 1: A_ik final through column k-1; lanes 2..: the front blocks of row i at stage k
-    const int* mine = nullptr;
-    int want = k;
-    if (lane == 0) {
-      mine = s.chain();
-      want = 2 * k + 2;
-    } else if (lane == 1) {
-      mine = s.ver(i, k);
-    } else if (lane < 2 + ncol && cols[lane - 2] <= i) {
-      mine = s.ver(i, cols[lane - 2]);
-    }
-    if (!wg_wait(s, mine, want, g.spin_limit)) return false;
+    // lane 0: D_k published; lane 1: A_ik final through column k-1 (the front blocks are waited for one by one below)
+    const int* mine = lane == 0 ? s.chain() : (lane == 1 ? s.ver(i, k) : nullptr);
+    if (!wg_wait(s, mine, lane == 0 ? 2 * k + 2 : k, g.spin_limit)) return false;
   }
   GPX_DAG_TASK_STAMP(idx, 2);
   tile_in(blk(i, k), lda, sA);
@@ -567,27 +618,37 @@ __device__ bool task_fr(const Args& g, double* A, double* Dinv, const Sync& s, i
   rowblock_out(acc, w, blk(i, k), lda, sA);
   wg_publish(t == 0 ? s.lrow(i) : nullptr, k + 1);
   GPX_DAG_TASK_STAMP(idx, 3);
-  // the diagonal block first (no wait), then the columns in order
-  for (int pass = 0; pass < 2; ++pass) {
-    for (int q = 0; q < ncol; ++q) {
-      const int j = cols[q];
-      if (j > i || (pass == 0) != (j == i)) continue;
-      tile_in(blk(i, j), lda, sB);
-      if (j == i) {
-        __syncthreads();
-        syrk_lower(sB, sA, w);
-        __syncthreads();
-        tile_out<true>(sB, blk(i, i), lda);
-      } else {
-        const int* mine = lane == 0 ? (j == k + 1 ? s.chain() : s.lrow(j)) : nullptr;
-        if (!wg_wait(s, mine, j == k + 1 ? 2 * k + 3 : k + 1, g.spin_limit)) return false;
-        tile_in(blk(j, k), lda, sX);
-        __syncthreads();
-        rowblock_sub_abt(acc, sB, sA, sX, w);
-        rowblock_out(acc, w, blk(i, j), lda, nullptr);
-      }
-      wg_publish(t == 0 ? s.ver(i, j) : nullptr, k + 1);
+  // front blocks in the order the chain needs them: column k+1 (the chain's next tile (k+2, k+1) when i = k+2), the
+  // diagonal block, then the others.  Each waits for its own version (the bulk tile of a column pair entering the
+  // front lands late in its stage) and, off the diagonal, for L_jk.
+  int order[3], nord = 0;
+  for (int q = 0; q < ncol; ++q)
+    if (cols[q] == k + 1 && cols[q] < i) order[nord++] = cols[q];
+  for (int q = 0; q < ncol; ++q)
+    if (cols[q] == i) order[nord++] = cols[q];
+  for (int q = 0; q < ncol; ++q)
+    if (cols[q] != k + 1 && cols[q] < i) order[nord++] = cols[q];
+  for (int q = 0; q < nord; ++q) {
+    const int j = order[q];
+    {
+      const int* mine = lane == 0 ? s.ver(i, j)
+                        : (lane == 1 && j != i) ? (j == k + 1 ? s.chain() : s.lrow(j)) : nullptr;
+      const int want = lane == 0 ? k : (j == k + 1 ? 2 * k + 3 : k + 1);
+      if (!wg_wait(s, mine, want, g.spin_limit)) return false;
     }
+    tile_in(blk(i, j), lda, sB);
+    if (j == i) {
+      __syncthreads();
+      syrk_lower(sB, sA, w);
+      __syncthreads();
+      tile_out<true>(sB, blk(i, i), lda);
+    } else {
+      tile_in(blk(j, k), lda, sX);
+      __syncthreads();
+      rowblock_sub_abt(acc, sB, sA, sX, w);
+      rowblock_out(acc, w, blk(i, j), lda, nullptr);
+    }
+    wg_publish(t == 0 ? s.ver(i, j) : nullptr, k + 1);
   }
   GPX_DAG_TASK_STAMP(idx, 4);
   return true;
@@ -632,22 +693,19 @@ __device__ bool task_update(const Args& g, double* A, const Sync& s, int i, int 
 
 __device__ void pool_role(const Args& g, double* A, double* Dinv, const Sync& s, double* lds) {
   __shared__ int s_ticket;
-  // front workers (blockIdx.x 1 .. front_workers) take the front list, then join the bulk list
-  int which = ((int)blockIdx.x <= g.front_workers && g.nfront > 0) ? 0 : 1;
+  // the critical and front workers take their own list, then join the bulk list
+  int which = (int)blockIdx.x < g.wend[0] ? 0 : ((int)blockIdx.x < g.wend[1] ? 1 : 2);
   for (;;) {
     if (threadIdx.x == 0)
       s_ticket = __hip_atomic_fetch_add(s.ticket(which), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     int idx = s_ticket;
     __syncthreads();
-    if (which == 0) {
-      if (idx >= g.nfront) {
-        which = 1;
-        continue;
-      }
-    } else {
-      idx += g.nfront;
-      if (idx >= g.ntasks) return;
+    idx += which ? g.lend[which - 1] : 0;
+    if (idx >= g.lend[which]) {
+      if (which == 2) return;
+      which = 2;
+      continue;
     }
     const unsigned long long code = g.tasks[idx];
     const int type = (int)(code & 0xff), a = (int)((code >> 8) & 0xff), b = (int)((code >> 16) & 0xff),
@@ -700,11 +758,13 @@ __global__ void __launch_bounds__(WG, 1) potrf_dag_kernel(Args g) {
 // is a topological order, which is all the device relies on (tools/dag_plan_check.hip: every list drains under a
 // worst-case in-order executor, for any number of workers).
 struct Plan {
-  std::vector<unsigned long long> list;  // front tasks, then bulk tasks
-  int nfront = 0, front_workers = 0;
+  std::vector<unsigned long long> list;  // critical tasks, front tasks, bulk tasks
+  int lend[3] = {0, 0, 0};                // list ends
+  int crit_workers = 0, front_workers = 0;
   unsigned long long* dev = nullptr;
   double sim_us = 0.0;
   std::vector<double> sim_chain;  // simulated start of each chain step (diagnostics)
+  double sim_busy_front = 0.0, sim_busy_bulk = 0.0;  // worker-microseconds busy
 };
 
 static unsigned long long encode(int type, int a, int b, int k0, int k1) {
@@ -727,6 +787,8 @@ static Plan simulate(int nblk, int P, int F) {
   const int kMinChunk = 4, kMaxChunk = 8;
   const double dt = 0.25, INF = 1e30;
   Plan plan;
+  const int CW = nblk >= 3 ? std::min(2, std::max(1, P - F - 1)) : 0;  // critical workers
+  plan.crit_workers = CW;
   plan.front_workers = F;
   const int M = nblk / 2;
   std::vector<double> verT((size_t)nblk * nblk * (nblk + 1), INF), lrowT((size_t)nblk * (nblk + 1), INF),
@@ -738,13 +800,19 @@ static Plan simulate(int nblk, int P, int F) {
     for (int j = 0; j <= i; ++j) VT(i, j, 0) = 0.0;
   }
   chainT[0] = 0.0;
+  // the critical list: FR(k+2, k), the only front task the chain's next step waits on; the front list: the others
   struct FTask { int type, i, j, k; };
-  std::vector<FTask> front;
-  for (int k = 0; k + 2 < nblk; ++k)
-    for (int i = k + 2; i < nblk; ++i) front.push_back({T_FR, i, k, k});
+  std::vector<FTask> crit, front;
+  for (int k = 0; k + 2 < nblk; ++k) {
+    crit.push_back({T_FR, k + 2, k, k});
+    for (int i = k + 3; i < nblk; ++i) front.push_back({T_FR, i, k, k});
+  }
+  for (const FTask& f : crit) plan.list.push_back(encode(T_FR, f.i, f.k, 0, 0));
+  plan.lend[0] = (int)plan.list.size();
   for (const FTask& f : front) plan.list.push_back(encode(T_FR, f.i, f.k, 0, 0));
-  plan.nfront = (int)front.size();
-  size_t fnext = 0;
+  plan.lend[1] = (int)plan.list.size();
+  std::vector<FTask> lists[2] = {crit, front};
+  size_t lnext[2] = {0, 0};
   struct BTile { int I, J, v; bool busy; };
   std::vector<BTile> tiles;
   for (int J = 2; J < M; ++J)
@@ -752,18 +820,15 @@ static Plan simulate(int nblk, int P, int F) {
   size_t bulk_left = tiles.size();
   int cstep = 0;
   double cfree = 0.0;
-  struct Worker { double free; int held; bool front; };  // held: front task waiting to start, or -1
+  // cls: 0 critical, 1 front, 2 bulk; held: the FR task the worker holds (index into lists[cls], -1: none); phase 0:
+  // waiting to start, 1 + q: front block q of its order next; tcur: when the task's previous phase ends
+  struct Worker { double free; int held; int cls; int phase; double tcur; };
   std::vector<Worker> wk(P);
-  for (int p = 0; p < P; ++p) wk[p] = {0.0, -1, p < F};
+  for (int p = 0; p < P; ++p) wk[p] = {0.0, -1, p < CW ? 0 : (p < CW + F ? 1 : 2), 0, 0.0};
   struct Ev { double t; int kind, a, b, v; };  // kind 0 chain word, 1 lrow, 2 version, 3 tile free
   std::vector<Ev> evs;
   auto front_ready = [&](const FTask& f, double now) {
-    int cols[3];
-    const int nc = front_cols(f.k, nblk, cols);
-    bool ok = chainT[2 * f.k + 2] <= now && VT(f.i, f.k, f.k) <= now && chainT[2 * f.k + 3] < INF;
-    for (int q = 0; q < nc; ++q)
-      if (cols[q] <= f.i) ok = ok && VT(f.i, cols[q], f.k) <= now;
-    return ok;
+    return chainT[2 * f.k + 2] <= now && VT(f.i, f.k, f.k) <= now;
   };
   double now = 0.0;
   for (long guard = 0; guard < 8000000; ++guard, now += dt) {
@@ -788,43 +853,66 @@ static Plan simulate(int nblk, int P, int F) {
       plan.sim_chain.push_back(now);
       ++cstep;
     }
+    {
+      int busy_b = 0, busy_f = 0;
+      for (const Worker& w : wk)
+        if (w.free > now) (w.cls < 2 ? busy_f : busy_b)++;
+      plan.sim_busy_front += busy_f * dt;
+      plan.sim_busy_bulk += busy_b * dt;
+    }
     bool front_busy = false;
     std::vector<int> idle;
     for (int p = 0; p < P; ++p) {
       Worker& w = wk[p];
       if (w.free > now) {
-        front_busy = front_busy || w.front;
+        front_busy = front_busy || w.cls < 2;
         continue;
       }
-      if (w.front && w.held < 0 && fnext < front.size()) w.held = (int)fnext++;
+      if (w.cls < 2 && w.held < 0) {
+        if (lnext[w.cls] < lists[w.cls].size()) {
+          w.held = (int)lnext[w.cls]++;
+          w.phase = 0;
+        } else {
+          w.cls = 2;  // joins the bulk
+        }
+      }
       if (w.held >= 0) {
         front_busy = true;
-        const FTask& f = front[w.held];
-        if (!front_ready(f, now)) continue;
-        // S part, then the diagonal block, then the columns as their L blocks become visible (estimated)
-        double tcur = now + cost.fr_s;
-        evs.push_back({tcur + cost.hop, 1, f.i, 0, f.k + 1});
+        const FTask& f = lists[w.cls][w.held];
+        if (w.phase == 0) {
+          if (!front_ready(f, now)) continue;
+          w.tcur = now + cost.fr_s;
+          evs.push_back({w.tcur + cost.hop, 1, f.i, 0, f.k + 1});
+          w.phase = 1;
+        }
+        // column k+1, the diagonal block, then the other front columns, each once its version (and L block) is
+        // known; the task holds the worker meanwhile, as on the device
         int cols[3];
         const int nc = front_cols(f.k, nblk, cols);
+        int order[3], nord = 0;
         for (int q = 0; q < nc; ++q)
-          if (cols[q] == f.i) {
-            tcur += cost.fr_u;
-            evs.push_back({tcur + cost.hop, 2, f.i, f.i, f.k + 1});
-          }
-        for (int q = 0; q < nc; ++q) {
-          const int j = cols[q];
-          if (j >= f.i) continue;
-          const double lvis = j == f.k + 1 ? chainT[2 * f.k + 3] : now + cost.fr_s + cost.hop;  // FR(j, k)'s S part
-          tcur = std::max(tcur, lvis) + cost.fr_u;
-          evs.push_back({tcur + cost.hop, 2, f.i, j, f.k + 1});
+          if (cols[q] == f.k + 1 && cols[q] < f.i) order[nord++] = cols[q];
+        for (int q = 0; q < nc; ++q)
+          if (cols[q] == f.i) order[nord++] = cols[q];
+        for (int q = 0; q < nc; ++q)
+          if (cols[q] != f.k + 1 && cols[q] < f.i) order[nord++] = cols[q];
+        while (w.phase - 1 < nord) {
+          const int j = order[w.phase - 1];
+          double ready = VT(f.i, j, f.k);
+          if (j != f.i) ready = std::max(ready, j == f.k + 1 ? chainT[2 * f.k + 3] : LT(j, f.k + 1));
+          if (ready > now) break;  // not visible yet (or not even scheduled)
+          w.tcur = std::max(w.tcur, ready) + cost.fr_u;
+          evs.push_back({w.tcur + cost.hop, 2, f.i, j, f.k + 1});
+          ++w.phase;
         }
-        w.free = tcur;
+        if (w.phase - 1 < nord) continue;
+        w.free = w.tcur;
         w.held = -1;
         continue;
       }
       idle.push_back(p);
     }
-    if (cstep >= nblk && fnext >= front.size() && !front_busy && bulk_left == 0) break;
+    if (cstep >= nblk && lnext[0] >= crit.size() && lnext[1] >= front.size() && !front_busy && bulk_left == 0) break;
     if (idle.empty() || bulk_left == 0) continue;
     struct Cand { double slack; int q, K; };
     std::vector<Cand> cands;
@@ -867,6 +955,7 @@ static Plan simulate(int nblk, int P, int F) {
       w.free = end;
     }
   }
+  plan.lend[2] = (int)plan.list.size();
   plan.sim_us = std::max(now, cfree);
   return plan;
 }
@@ -876,7 +965,7 @@ static Plan build_plan(int nblk, int P) {
   best.sim_us = 1e30;
   for (int div : {8, 6, 4, 3}) {
     const int F = std::max(1, std::min(nblk, P / div));
-    if (F >= P) continue;
+    if (F + 3 > P) continue;
     Plan p = simulate(nblk, P, F);
     if (p.sim_us < best.sim_us) best = std::move(p);
   }
@@ -969,9 +1058,9 @@ hipError_t launch_potrf_dag(Context* c, int npad, double* A, int64_t lda, double
   g.sw = bt.w;
   g.ss = dag::sync_words(nblk);
   g.tasks = plan.dev;
-  g.ntasks = (int)plan.list.size();
-  g.nfront = plan.nfront;
-  g.front_workers = plan.front_workers;
+  for (int q = 0; q < 3; ++q) g.lend[q] = plan.lend[q];
+  g.wend[0] = 1 + plan.crit_workers;
+  g.wend[1] = 1 + plan.crit_workers + plan.front_workers;
   g.spin_limit = c->spin_limit;
   dag::potrf_dag_kernel<<<dim3(G, bt.count), WG, 0, c->stream>>>(g);
   return hipGetLastError();

@@ -1,5 +1,5 @@
 // CPU check of the dataflow Cholesky's task lists (tools/, no GPU): for every list, a worst-case executor with P
-// workers that take tasks strictly in list order and block on unmet dependencies must drain the graph, and every
+// workers that take tasks strictly in the order of their lists and block on unmet dependencies must drain the graph, and every
 // 64-block must receive its stages exactly once, in order.  Also prints the simulated makespan.
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -13,29 +13,30 @@ static bool check(int nblk, int P, bool verbose) {
   const int nt = (int)plan.list.size();
   std::vector<int> state(nt, 0);  // 0 not taken, 1 taken (blocked or running), 2 done; FR: 3 = S part done
   int cstep = 0;
-  // two pools as on the device: F front workers take the front list [0, nfront), then join the bulk list
-  const int F = plan.front_workers, nf = plan.nfront;
-  int fnext = 0, bnext = nf;
-  std::vector<int> held;  // tasks held by workers
-  std::vector<int> hfront;  // workers still on the front list
+  // three pools as on the device: CW critical workers take [0, lend[0]), F front workers [lend[0], lend[1]); each
+  // joins the bulk list [lend[1], lend[2]) once its own list is empty; the other workers take the bulk list
+  const int CW = plan.crit_workers, F = plan.front_workers;
+  int next[3] = {0, plan.lend[0], plan.lend[1]};
+  struct Wk { int cls, held; };
+  std::vector<Wk> wk(P);
+  for (int p = 0; p < P; ++p) wk[p] = {p < CW ? 0 : (p < CW + F ? 1 : 2), -1};
   auto dec = [&](int q, int& type, int& a, int& b, int& k0, int& k1) {
     const unsigned long long c = plan.list[q];
     type = c & 0xff; a = (c >> 8) & 0xff; b = (c >> 16) & 0xff; k0 = (c >> 24) & 0xff; k1 = (c >> 32) & 0xff;
   };
   for (int iter = 0;; ++iter) {
     bool progress = false;
-    // front workers (F of the P) hold front tasks while any remain; the rest hold bulk tasks
-    {
-      int nfront_held = 0;
-      for (int q : held) nfront_held += q < nf;
-      while ((int)held.size() < P) {
-        const bool front_slot = nfront_held < F && fnext < nf;
-        if (front_slot) { held.push_back(fnext); state[fnext++] = 1; ++nfront_held; progress = true; continue; }
-        // a worker that is not holding a front task: bulk (front workers join once the front list is empty)
-        const int bulk_workers = P - (fnext < nf ? F : nfront_held);
-        int nbulk_held = (int)held.size() - nfront_held;
-        if (bnext < nt && nbulk_held < bulk_workers) { held.push_back(bnext); state[bnext++] = 1; progress = true; continue; }
-        break;
+    for (Wk& w : wk) {
+      while (w.held < 0) {
+        if (next[w.cls] < plan.lend[w.cls]) {
+          w.held = next[w.cls]++;
+          state[w.held] = 1;
+          progress = true;
+        } else if (w.cls < 2) {
+          w.cls = 2;
+        } else {
+          break;
+        }
       }
     }
     // chain step
@@ -52,8 +53,9 @@ static bool check(int nblk, int P, bool verbose) {
         progress = true;
       }
     }
-    for (size_t h = 0; h < held.size();) {
-      const int q = held[h];
+    for (Wk& w : wk) {
+      if (w.held < 0) continue;
+      const int q = w.held;
       int type, a, b, k0, k1;
       dec(q, type, a, b, k0, k1);
       bool done = false;
@@ -61,38 +63,32 @@ static bool check(int nblk, int P, bool verbose) {
         const int i = a, k = b;
         int cols[3];
         const int nc = front_cols(k, nblk, cols);
+        int order[3], nord = 0;
+        for (int c2 = 0; c2 < nc; ++c2)
+          if (cols[c2] == k + 1 && cols[c2] < i) order[nord++] = cols[c2];
+        for (int c2 = 0; c2 < nc; ++c2)
+          if (cols[c2] == i) order[nord++] = cols[c2];
+        for (int c2 = 0; c2 < nc; ++c2)
+          if (cols[c2] != k + 1 && cols[c2] < i) order[nord++] = cols[c2];
         if (state[q] == 1) {
-          bool ok = chain >= 2 * k + 2 && ver[i * nblk + k] >= k;
-          for (int c2 = 0; c2 < nc; ++c2)
-            if (cols[c2] <= i) ok = ok && ver[i * nblk + cols[c2]] >= k;
-          if (ok) {
+          if (chain >= 2 * k + 2 && ver[i * nblk + k] >= k) {
             if (ver[i * nblk + k] != k) { printf("FR(%d,%d) tile version %d\n", i, k, ver[i * nblk + k]); return false; }
             lrow[i] = k + 1;
             ver[i * nblk + k] = k + 1;  // L final
-            state[q] = 3;                 // then the front blocks: 3 = diagonal pending, 4 + c2 = column c2 pending
+            state[q] = 4;               // 4 + q: front block order[q] pending
             progress = true;
           }
         }
-        if (state[q] == 3) {
-          for (int c2 = 0; c2 < nc; ++c2)
-            if (cols[c2] == i) {
-              if (ver[i * nblk + i] != k) { printf("FR(%d,%d) diag version %d\n", i, k, ver[i * nblk + i]); return false; }
-              ver[i * nblk + i] = k + 1;
-            }
-          state[q] = 4;
-          progress = true;
-        }
-        while (state[q] >= 4 && state[q] - 4 < nc) {
-          const int j = cols[state[q] - 4];
-          if (j >= i) { ++state[q]; continue; }
-          const bool lok = j == k + 1 ? cstep >= k + 2 : lrow[j] >= k + 1;
-          if (!lok) break;
+        while (state[q] >= 4 && state[q] - 4 < nord) {
+          const int j = order[state[q] - 4];
+          if (ver[i * nblk + j] < k) break;
+          if (j != i && !(j == k + 1 ? cstep >= k + 2 : lrow[j] >= k + 1)) break;
           if (ver[i * nblk + j] != k) { printf("FR(%d,%d) column %d version %d\n", i, k, j, ver[i * nblk + j]); return false; }
           ver[i * nblk + j] = k + 1;
           ++state[q];
           progress = true;
         }
-        if (state[q] >= 4 && state[q] - 4 >= nc) done = true;
+        if (state[q] >= 4 && state[q] - 4 >= nord) done = true;
       } else {
         const int R = type == T_U64 ? 1 : 2;
         bool ok = true;
@@ -111,11 +107,13 @@ static bool check(int nblk, int P, bool verbose) {
           done = true;
         }
       }
-      if (done) { state[q] = 2; held[h] = held.back(); held.pop_back(); progress = true; }
-      else ++h;
+      if (done) { state[q] = 2; w.held = -1; progress = true; }
     }
-    if (fnext >= nf && bnext >= nt && held.empty() && cstep >= nblk) break;
-    if (!progress) { printf("DEADLOCK nblk=%d P=%d F=%d at front %d/%d bulk %d/%d chain step %d\n", nblk, P, F, fnext, nf, bnext, nt, cstep); return false; }
+    bool idle = cstep >= nblk;
+    for (const Wk& w : wk) idle = idle && w.held < 0;
+    for (int c = 0; c < 3; ++c) idle = idle && next[c] >= plan.lend[c];
+    if (idle) break;
+    if (!progress) { printf("DEADLOCK nblk=%d P=%d CW=%d F=%d at lists %d %d %d chain step %d\n", nblk, P, CW, F, next[0], next[1], next[2], cstep); return false; }
   }
   // every block (i, j), i > j: versions reach j + 1 (L final), diagonal: j
   for (int i = 0; i < nblk; ++i)
@@ -128,7 +126,7 @@ static bool check(int nblk, int P, bool verbose) {
   if (verbose) {
     int cnt[4] = {0};
     for (auto c : plan.list) cnt[c & 0xff]++;
-    printf("nblk=%d P=%d F=%d: %d tasks (FR %d, U64 %d, U128 %d), simulated %.1f us\n", nblk, P, plan.front_workers, (int)plan.list.size(), cnt[1], cnt[2], cnt[3], plan.sim_us);
+    printf("nblk=%d P=%d CW=%d F=%d: %d tasks (FR %d, U64 %d, U128 %d), simulated %.1f us\n", nblk, P, plan.crit_workers, plan.front_workers, (int)plan.list.size(), cnt[1], cnt[2], cnt[3], plan.sim_us);
   }
   return true;
 }
@@ -139,7 +137,8 @@ int main() {
     for (int P : {7, 15, 31, 63, 127, 255}) ok = check(nblk, P, P == 255 || P == 63) && ok;
   for (int P : {255, 63}) {
     Plan pl = build_plan(64, P);
-    printf("P=%d F=%d simulated chain starts:", P, pl.front_workers);
+    printf("P=%d F=%d busy: front %.0f of %.0f, bulk %.0f of %.0f worker-us; chain starts:", P, pl.front_workers,
+           pl.sim_busy_front, pl.front_workers * pl.sim_us, pl.sim_busy_bulk, (P - pl.front_workers) * pl.sim_us);
     for (size_t c = 0; c < pl.sim_chain.size(); c += 4) printf(" %.0f", pl.sim_chain[c]);
     printf("\n");
   }

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <vector>
 #include <algorithm>
 #include <cmath>
@@ -165,6 +166,18 @@ int main(int argc, char** argv) {
         kb[K] += (tk[q][1] - tk[q][2]) * 0.01;
         kc[K] += 1;
       }
+    // the critical hand-off: chain step c publishes L_{c,c-1} (after pivot block 0), FR(c+1, c-1) (critical list entry
+    // c-1) updates A_{c+1,c} and A_{c+1,c+1}, the chain loads them after its step; times relative to step c's start
+    printf("critical FR(c+1,c-1) vs chain step c (us from step start): L_{c,c-1} pub | FR taken, deps met, L_ik pub, "
+           "end | chain out, next ready\n");
+    for (int c = 2; c + 1 < nblk; c += std::max(1, nblk / 12)) {
+      const int q = c - 1;
+      if (q >= plan.lend[0]) break;
+      const double b0 = (double)ch[c][0];
+      auto rel = [&](unsigned long long x) { return ((double)x - b0) * 0.01; };
+      printf("  c=%2d: %6.2f | %7.2f %7.2f %7.2f %7.2f | %6.2f %6.2f\n", c, rel(ch[c][3]), rel(tk[q][0]), rel(tk[q][2]),
+             rel(tk[q][3]), rel(tk[q][1]), rel(ch[c][8]), rel(ch[c][9]));
+    }
     for (int K = 1; K <= 8; ++K) if (kc[K] > 0) printf("  U128 K=%d: %4.0f tasks, running avg %.2f us\n", K, kc[K], kb[K] / kc[K]);
   }
   // timing
@@ -198,12 +211,27 @@ int main(int argc, char** argv) {
     bt.k = (int64_t)n * n;
     bt.dinv = 2 * nblk * NB * NB;
     printf("batched workers per problem: %d\n", potrf_dag_workers(&ctx, n, batch));
-    float ms;
-    CK(hipEventRecord(e0, ctx.stream));
+    // the first call builds the plan (host simulation); time the later ones, each on fresh copies of the Grams
+    float ms = 1e9;
+    double* Ab = nullptr;
+    CK(hipMalloc(&Ab, bytes * batch));
+    CK(hipMemcpy(Ab, A, bytes * batch, hipMemcpyDeviceToDevice));
+    auto t0 = std::chrono::steady_clock::now();
     run(2, A, D, bt);
-    CK(hipEventRecord(e1, ctx.stream));
-    CK(hipEventSynchronize(e1));
-    CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipStreamSynchronize(ctx.stream));
+    printf("batched first call (plan build + factor): %.3f ms\n",
+           std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    for (int r = 0; r < std::max(1, reps); ++r) {
+      CK(hipMemcpy(A, Ab, bytes * batch, hipMemcpyDeviceToDevice));
+      float m;
+      CK(hipEventRecord(e0, ctx.stream));
+      run(2, A, D, bt);
+      CK(hipEventRecord(e1, ctx.stream));
+      CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&m, e0, e1));
+      ms = std::min(ms, m);
+    }
+    CK(hipFree(Ab));
     std::vector<int32_t> hi(batch);
     CK(hipMemcpy(hi.data(), info, 4 * batch, hipMemcpyDeviceToHost));
     int mism = 0;
@@ -218,7 +246,7 @@ int main(int argc, char** argv) {
       for (int i = 0; i < n; ++i)
         for (int j = 0; j <= i; ++j) mism += memcmp(&Lb[(size_t)i * n + j], &Ls[(size_t)i * n + j], 8) != 0;
     }
-    printf("batched x%d: %.3f ms, info %d %d.., lower entries differing from single fits: %d\n", batch, ms, hi[0],
+    printf("batched x%d: best %.3f ms, info %d %d.., lower entries differing from single fits: %d\n", batch, ms, hi[0],
            batch > 1 ? hi[1] : 0, mism);
   }
   // NOT_PD: a negative diagonal entry deep inside

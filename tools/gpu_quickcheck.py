@@ -21,6 +21,7 @@ def run(n, d, kind, m, nrhs=1, seed=0):
     L = torch.tril(st.L).cpu().numpy()[:n,:n]
     Lref = O.cholesky(Kref)
     print(f"  chol max|dL| = {np.abs(L-Lref).max():.3e}  info={int(st.info.item())}")
+    eng.inverse(st)  # a factor-only update leaves W unbuilt (GPState.W_ready False); build it before reading
     W = st.W.cpu().numpy()
     Winv_ref = np.linalg.inv(Lref).T
     print(f"  W max|dW| (upper) = {np.abs(np.triu(W[:n,:n]) - Winv_ref).max():.3e}, max|W|={np.abs(Winv_ref).max():.3e}")
