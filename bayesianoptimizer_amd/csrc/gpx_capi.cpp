@@ -279,7 +279,8 @@ gpx_status gpx_gram_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, con
 }
 
 static gpx_status potrf_impl(gpx_handle h, int64_t n, double* A, int64_t lda, double* Dinv, int32_t* info,
-                             bool clear_info, double* W = nullptr, int64_t ldw = 0) {
+                             bool clear_info, double* W = nullptr, int64_t ldw = 0,
+                             const gpx::ForwardRhs* fr = nullptr, bool* z_done = nullptr) {
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return GPX_INVALID_ARG;
   GPX_TRY(check_n(c, n));
@@ -290,7 +291,7 @@ static gpx_status potrf_impl(gpx_handle h, int64_t n, double* A, int64_t lda, do
   GPX_TRY(check_ld(c, lda, npad, "A", true));
   GPX_USE_DEVICE(c);
   if (clear_info) GPX_TRY(hip_check(c, hipMemsetAsync(info, 0, sizeof(int32_t), c->stream), "memset info"));
-  return hip_check(c, gpx::launch_potrf(c, (int)npad, A, lda, Dinv, info, gpx::Batch(), W, ldw), "potrf");
+  return hip_check(c, gpx::launch_potrf(c, (int)npad, A, lda, Dinv, info, gpx::Batch(), W, ldw, fr, z_done), "potrf");
 }
 
 gpx_status gpx_potrf_f64(gpx_handle h, int64_t n, double* A, int64_t lda, double* Dinv, int32_t* info) {
@@ -444,7 +445,7 @@ gpx_status gpx_potrs_workspace_size(int64_t n, int64_t nrhs, size_t* bytes) {
 
 static gpx_status potrs_impl(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv,
                              const double* Y, int64_t ldy, int64_t nrhs, double const_mean, double* alpha,
-                             int32_t* info, void* ws, size_t ws_bytes, bool ws_cleared);
+                             int32_t* info, void* ws, size_t ws_bytes, bool ws_cleared, const double* z = nullptr);
 
 gpx_status gpx_potrs_f64(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv, const double* Y,
                          int64_t ldy, int64_t nrhs, double const_mean, double* alpha, int32_t* info, void* ws,
@@ -454,7 +455,7 @@ gpx_status gpx_potrs_f64(gpx_handle h, int64_t n, const double* L, int64_t ldl, 
 
 static gpx_status potrs_impl(gpx_handle h, int64_t n, const double* L, int64_t ldl, const double* Dinv,
                              const double* Y, int64_t ldy, int64_t nrhs, double const_mean, double* alpha,
-                             int32_t* info, void* ws, size_t ws_bytes, bool ws_cleared) {
+                             int32_t* info, void* ws, size_t ws_bytes, bool ws_cleared, const double* z) {
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return GPX_INVALID_ARG;
   GPX_TRY(check_n(c, n));
@@ -472,7 +473,7 @@ static gpx_status potrs_impl(gpx_handle h, int64_t n, const double* L, int64_t l
   if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "potrs workspace too small");
   GPX_USE_DEVICE(c);
   return hip_check(c, gpx::launch_potrs(c, (int)n, (int)npad, L, ldl, Dinv, Y, ldy, (int)nrhs, const_mean, alpha, info,
-                                        align256(ws), gpx::Batch(), ws_cleared),
+                                        align256(ws), gpx::Batch(), ws_cleared, z),
                    "potrs");
 }
 
@@ -491,10 +492,23 @@ gpx_status gpx_fit_factor_f64(gpx_handle h, const gpx_kernel_params* p, int64_t 
   if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "fit workspace too small");
   if (!info) return fail(c, GPX_INVALID_ARG, "info is NULL");
   if (!ws) return fail(c, GPX_INVALID_ARG, "ws is NULL");
+  GPX_NONNULL(c, Y);
+  GPX_TRY(check_ld(c, ldy, nrhs, "Y", false));
   // the Gram launch also clears the triangular solve's hand-off granules (no memset dispatch)
-  GPX_TRY(gram_impl(h, p, n, X, ldx, K, ldk, info, align256(ws), gpx::potrs_clear_bytes(padded(n), nrhs, 1)));
-  GPX_TRY(potrf_impl(h, n, K, ldk, Dinv, info, false));
-  return potrs_impl(h, n, K, ldk, Dinv, Y, ldy, nrhs, p->const_mean, alpha, info, ws, ws_bytes, true);
+  const int64_t npad = padded(n);
+  GPX_TRY(gram_impl(h, p, n, X, ldx, K, ldk, info, align256(ws), gpx::potrs_clear_bytes(npad, nrhs, 1)));
+  // the dataflow Cholesky also runs the forward substitution; the solve is then its backward half
+  gpx::ForwardRhs fr;
+  fr.Y = Y;
+  fr.ldy = ldy;
+  fr.nrhs = (int)nrhs;
+  fr.n = (int)n;
+  fr.mean = p->const_mean;
+  fr.buf = reinterpret_cast<double*>(reinterpret_cast<char*>(align256(ws)) + gpx::potrs_forward_offset(npad, nrhs, 1));
+  bool z_done = false;
+  GPX_TRY(potrf_impl(h, n, K, ldk, Dinv, info, false, nullptr, 0, &fr, &z_done));
+  return potrs_impl(h, n, K, ldk, Dinv, Y, ldy, nrhs, p->const_mean, alpha, info, ws, ws_bytes, true,
+                    z_done ? fr.buf + npad * gpx::rhs_row((int)nrhs) : nullptr);
 }
 
 gpx_status gpx_append_workspace_size(int64_t n_old, int64_t n_new, int64_t nrhs, size_t* bytes) {
@@ -610,11 +624,24 @@ static gpx_status fit_batched_impl(gpx_handle h, const gpx_kernel_params* p, int
                                         inverse ? nullptr : slice,
                                         inverse ? 0 : gpx::potrs_clear_bytes(npad, nrhs, batch)),
                     "gram"));
-  GPX_TRY(hip_check(c, gpx::launch_potrf(c, (int)npad, K, ldk, Dinv, info, bt, W, ldw), "potrf"));
-  if (!inverse)
+  if (!inverse) {
+    // factor + forward substitution (dataflow schedule), then the backward half of the solve
+    gpx::ForwardRhs fr;
+    fr.Y = Y;
+    fr.ldy = ldy;
+    fr.sy = stride_y;
+    fr.nrhs = (int)nrhs;
+    fr.n = (int)n;
+    fr.mean = p->const_mean;
+    fr.buf = reinterpret_cast<double*>(reinterpret_cast<char*>(slice) + gpx::potrs_forward_offset(npad, nrhs, batch));
+    bool z_done = false;
+    GPX_TRY(hip_check(c, gpx::launch_potrf(c, (int)npad, K, ldk, Dinv, info, bt, nullptr, 0, &fr, &z_done), "potrf"));
+    const int64_t nr = gpx::rhs_row((int)nrhs);
     return hip_check(c, gpx::launch_potrs(c, (int)n, (int)npad, K, ldk, Dinv, Y, ldy, (int)nrhs, p->const_mean, alpha,
-                                          info, slice, bt, true),
+                                          info, slice, bt, true, z_done ? fr.buf + npad * nr : nullptr, 2 * npad * nr),
                      "potrs");
+  }
+  GPX_TRY(hip_check(c, gpx::launch_potrf(c, (int)npad, K, ldk, Dinv, info, bt, W, ldw), "potrf"));
   GPX_TRY(hip_check(c, gpx::launch_trtri(c, (int)npad, K, ldk, Dinv, W, ldw, slice, bt, true), "trtri"));
   double* zpart = slice;
   double* z = zpart + (size_t)(npad / 128) * npad * nrhs;

@@ -90,15 +90,28 @@ struct Batch {
 hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
                        double* K, int64_t ldk, const Batch& bt = Batch(), int rb0 = 0, int32_t* info = nullptr,
                        void* zero = nullptr, size_t zero_bytes = 0);
+// The forward half of alpha's triangular solve folded into the dataflow Cholesky: z = L^{-1} (Y - mean), with the
+// padded rows and right-hand sides >= nrhs at 0.  buf (per problem, stride 2 npad nr doubles): the running right-hand
+// sides (npad x nr), then z (npad x nr); nr = 1 for one right-hand side, else GPX_MAX_RHS (potrs' layout).
+struct ForwardRhs {
+  const double* Y = nullptr;
+  int64_t ldy = 0, sy = 0;  // sy: Y stride per problem
+  int nrhs = 1, n = 0;
+  double mean = 0.0;
+  double* buf = nullptr;
+};
+inline int rhs_row(int nrhs) { return nrhs == 1 ? 1 : GPX_MAX_RHS; }
 // W (optional): the Dinv pass also writes W's diagonal blocks D_k^T (what trtri_diag would), so a fit that follows
-// with launch_trtri(..., diag_done = true) saves one dispatch.
+// with launch_trtri(..., diag_done = true) saves one dispatch.  fr (optional): fold the forward substitution into the
+// factorisation where the dataflow schedule runs; *z_done tells whether it did (z = buf + npad nr per problem).
 hipError_t launch_potrf(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info,
-                        const Batch& bt = Batch(), double* W = nullptr, int64_t ldw = 0);
+                        const Batch& bt = Batch(), double* W = nullptr, int64_t ldw = 0,
+                        const ForwardRhs* fr = nullptr, bool* z_done = nullptr);
 // the persistent dataflow schedule for npad <= 4096 (gpx_potrf_dag.hip); launch_potrf uses it when
 // potrf_dag_workers() > 0
 int potrf_dag_workers(Context* c, int npad, int batch);
 hipError_t launch_potrf_dag(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info,
-                            const Batch& bt, double* W, int64_t ldw);
+                            const Batch& bt, double* W, int64_t ldw, const ForwardRhs* fr = nullptr);
 void potrf_dag_release(Context* c);
 hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, const double* Dinv, double* W,
                         int64_t ldw, double* T, const Batch& bt = Batch(), bool diag_done = false);
@@ -110,9 +123,14 @@ hipError_t launch_alpha(Context* c, int n, int npad, const double* W, int64_t ld
 size_t potrs_workspace_bytes(int64_t npad, int64_t nrhs, int64_t batch);
 // ws_cleared: the granule block (potrs_clear_bytes) was already zeroed on the stream (by launch_gram in a fit)
 size_t potrs_clear_bytes(int64_t npad, int64_t nrhs, int64_t batch);
+// byte offset in the potrs workspace of the ForwardRhs buffer (2 npad nr doubles per problem)
+size_t potrs_forward_offset(int64_t npad, int64_t nrhs, int64_t batch);
+// z (optional): z = L^{-1} (Y - mean) from the factorisation (ForwardRhs; per problem at z + b * sz): the backward half
+// only
 hipError_t launch_potrs(Context* c, int n, int npad, const double* L, int64_t ldl, const double* Dinv,
                         const double* Y, int64_t ldy, int nrhs, double const_mean, double* alpha,
-                        int32_t* info, void* ws, const Batch& bt = Batch(), bool ws_cleared = false);
+                        int32_t* info, void* ws, const Batch& bt = Batch(), bool ws_cleared = false,
+                        const double* z = nullptr, int64_t sz = 0);
 
 struct SweepBuffers {
   double* kstar;     // npad x C

@@ -532,11 +532,15 @@ static void launch_dinv(Context* ctx, int nblk, double* A, int64_t lda, double* 
 }
 
 hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
-                        double* W, int64_t ldw) {
+                        double* W, int64_t ldw, const ForwardRhs* fr, bool* z_done) {
   LaunchTimer tm(ctx, GPX_TIMER_POTRF);
   const int nblk = npad / NB;
-  if (ctx->potrf_schedule != 1 && potrf_dag_workers(ctx, npad, bt.count) > 0)
-    return launch_potrf_dag(ctx, npad, A, lda, Dinv, info, bt, W, ldw);
+  if (z_done) *z_done = false;
+  if (ctx->potrf_schedule != 1 && potrf_dag_workers(ctx, npad, bt.count) > 0) {
+    hipError_t e = launch_potrf_dag(ctx, npad, A, lda, Dinv, info, bt, W, ldw, fr);
+    if (e == hipSuccess && z_done && fr && fr->Y) *z_done = true;
+    return e;
+  }
   launch_steps(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk);
   launch_dinv(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, W, ldw);
   return hipGetLastError();

@@ -235,9 +235,139 @@ __device__ __forceinline__ void rowblock_out(const d4 (&acc)[4], int w, double* 
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int row = 16 * w + (lane >> 4) + 4 * q, col = 16 * bj + (lane & 15);
-      st1(r, (int)(((int64_t)row * ld + col) * 8), acc[bj][q]);
+      if (G) st1(r, (int)(((int64_t)row * ld + col) * 8), acc[bj][q]);
       if (S) S[row * LD + col] = acc[bj][q];
     }
+}
+
+// Rows 0..15 of an LDS tile -> global (sc1), by waves 1-3 (the chain's S row of wave 0)
+__device__ __forceinline__ void rows16_out(const double* S, double* G, int64_t ld) {
+  const rsrc_t r = rsrc(G);
+  for (int e = threadIdx.x - 64; e < 16 * 32; e += WG - 64) {
+    const int row = e >> 5, col = 2 * (e & 31);
+    st2(r, (int)(((int64_t)row * ld + col) * 8), S[row * LD + col], S[row * LD + col + 1]);
+  }
+}
+
+// ---- forward substitution folded into the factorisation -----------------------------------------------------------
+// z = L^{-1} b, b = Y - mean (0 on padded rows / right-hand sides), block row by block row: y_i = b_i - sum_{k<i} L_ik z_k
+// accumulates in stage order (FR(i, k) applies stage k right after its L_ik, before it publishes anything that lets
+// stage k+1 of row i start; the chain applies stage c-1 of row c after its S), and z_c = D_c y_c.  The triangular solve
+// then runs its backward half only (gpx_potrs.hip).  Right-hand sides are rows of NR doubles (NR = 1, or GPX_MAX_RHS).
+struct Fwd {
+  const double* Y;  // nullptr: no forward substitution in this launch
+  int64_t ldy, sy, sf;  // sy: Y stride per problem; sf: yb / zb stride per problem
+  int nrhs, n, nr;
+  double mean;
+  double* yb;  // running right-hand sides, npad x nr (written and read in this launch: sc1)
+  double* zb;  // z, npad x nr
+  // this problem's arrays (read from the kernel arguments where they are used: no registers held across the tasks)
+  __device__ const double* y_in() const { return Y + (int64_t)blockIdx.y * sy; }
+  __device__ double* ybuf() const { return yb + (int64_t)blockIdx.y * sf; }
+  __device__ double* zbuf() const { return zb + (int64_t)blockIdx.y * sf; }
+};
+
+__device__ __forceinline__ double rhs_b(const Fwd& f, int row, int rr) {
+  return (row < f.n && rr < f.nrhs) ? f.y_in()[(int64_t)row * f.ldy + rr] - f.mean : 0.0;
+}
+
+// The 16-row layout of a wave: lane = 4 i + q (row i of the block, quarter q of the 64 columns).  The lane's own
+// right-hand sides after the reduction: NR = 1: q = 0 holds rr 0; NR = 8: lane q holds rr 2q and 2q+1.
+template <int NR>
+__device__ __forceinline__ int own_rr(int q, int e) {
+  return NR == 1 ? ((q == 0 && e == 0) ? 0 : -1) : 2 * q + e;
+}
+
+// The lane's two sums of own_rr of row i of a 16-row block, sum_j M(i, j) x(j, rr) (M rows in LDS with row stride LD,
+// x in LDS as 64 x NR): lane (i, q) sums j in [16q, 16q + 16) (LOWER: only column blocks q <= rowblk), then the four
+// partials of a row are combined by a reduce-scatter over lanes q ^ 2 and q ^ 1 (NR = 8) or two xor shuffles (NR = 1):
+// every sum in one fixed order, without indexing registers by lane.
+template <int NR, bool LOWER>
+__device__ __forceinline__ void gemv16(double (&out)[2], const double* M, const double* x, int rowblk) {
+  const int lane = threadIdx.x & 63, i = lane >> 2, q = lane & 3;
+  double p[NR];
+#pragma unroll
+  for (int rr = 0; rr < NR; ++rr) p[rr] = 0.0;
+  if (!LOWER || q <= rowblk) {
+#pragma unroll 4
+    for (int jj = 0; jj < 16; ++jj) {
+      const int j = 16 * q + jj;
+      const double m = M[i * LD + j];
+#pragma unroll
+      for (int rr = 0; rr < NR; ++rr) p[rr] = fma(m, x[j * NR + rr], p[rr]);
+    }
+  }
+  if constexpr (NR == 1) {
+    p[0] += __shfl_xor(p[0], 1);
+    p[0] += __shfl_xor(p[0], 2);
+    out[0] = p[0];
+    out[1] = 0.0;
+  } else {
+    static_assert(NR == 8, "one or eight right-hand sides");
+    const bool hi2 = (q & 2) != 0, hi1 = (q & 1) != 0;
+    double a[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double keep = hi2 ? p[j + 4] : p[j], send = hi2 ? p[j] : p[j + 4];
+      a[j] = keep + __shfl_xor(send, 2);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const double keep = hi1 ? a[j + 2] : a[j], send = hi1 ? a[j] : a[j + 2];
+      out[j] = keep + __shfl_xor(send, 1);
+    }
+  }
+}
+
+// The lane's two y values of row `row` (global): from b on the row's first stage, else from yb (sc1)
+template <int NR>
+__device__ __forceinline__ void load_y(const Fwd& f, int row, bool first, double (&y)[2]) {
+  const int q = threadIdx.x & 3;
+  const rsrc_t r = rsrc(f.ybuf());
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int rr = own_rr<NR>(q, e);
+    y[e] = 0.0;
+    if (rr >= 0) y[e] = first ? rhs_b(f, row, rr) : ld1(r, (int)(((int64_t)row * NR + rr) * 8));
+  }
+}
+
+// y -= L z on the wave's 16 rows (L rows in LDS), the result into yb (sc1) or LDS (ys: 64 x NR, row i0 + i)
+template <int NR>
+__device__ __forceinline__ void fwd_rows16(const Fwd& f, const double* Lrows, const double* zs, double (&y)[2], int row,
+                                           double* ys, int i0) {
+  const int lane = threadIdx.x & 63, i = lane >> 2, q = lane & 3;
+  double p[2];
+  gemv16<NR, false>(p, Lrows, zs, 0);
+  const rsrc_t r = rsrc(f.ybuf());
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int rr = own_rr<NR>(q, e);
+    if (rr < 0) continue;
+    const double v = y[e] - p[e];
+    if (ys)
+      ys[(i0 + i) * NR + rr] = v;
+    else
+      st1(r, (int)(((int64_t)row * NR + rr) * 8), v);
+  }
+}
+
+// z rows of 16-row block rb of chain block c: z = D y (D in LDS, y in LDS 64 x NR) -> zs (LDS) and zb (sc1)
+template <int NR>
+__device__ __forceinline__ void z_rows16(const Fwd& f, const double* D, const double* ys, int c, int rb, double* zs) {
+  const int lane = threadIdx.x & 63, i = lane >> 2, q = lane & 3;
+  double p[2];
+  gemv16<NR, true>(p, D + 16 * rb * LD, ys, rb);
+  const rsrc_t r = rsrc(f.zbuf());
+  const int row = 16 * rb + i;
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int rr = own_rr<NR>(q, e);
+    if (rr < 0) continue;
+    const double v = p[e];
+    if (zs) zs[row * NR + rr] = v;
+    st1(r, (int)(((int64_t)(c * NB + row) * NR + rr) * 8), v);
+  }
 }
 
 // ---- one step of the chain ---------------------------------------------------------------------------------------
@@ -252,7 +382,7 @@ __device__ __forceinline__ void rowblock_out(const d4 (&acc)[4], int w, double* 
 //      final through column c-1 and, once they are, load them into sB / sN (the 64 x 128 strip, one third per wave).
 // Out: sA = L_cc (lower 16-blocks), sX = D_c.  Returns the failing pivot 0..63 or -1, uniform; *pref == 3: prefetched.
 struct ChainShared {
-  int cnt, srow, fail, pref, prefdone, pub;
+  int cnt, srow, fail, pref, prefdone, pub, zcnt;
 };
 
 __device__ __forceinline__ void prefetch_share(const double* strip, int64_t ld, double* sB, double* sN, int w) {
@@ -310,7 +440,7 @@ __device__ __forceinline__ void store_prev(const double* sL, const double* sD, d
 
 __device__ __forceinline__ int chain_step(const Sync& s, int c, int nblk, double* A, int64_t lda, double* Dinv,
                                           double* W, int64_t ldw, double* sA, double* sB, double* sX, double* sN,
-                                          ChainShared& sh) {
+                                          ChainShared& sh, const Fwd& fw, double* fl) {
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   auto dblk = [&](int q) { return sX + 16 * q * LD + 16 * q; };
   auto tsolve = [&](int i, int q) {
@@ -368,9 +498,39 @@ __device__ __forceinline__ int chain_step(const Sync& s, int c, int nblk, double
     sh.pref = 0;
     sh.prefdone = 0;
     sh.pub = 0;
+    sh.zcnt = 0;
   }
   __syncthreads();
+  // forward substitution: y blocks of waves 1-3 (wave 1: 16-row blocks 0 and 1, waves 2 / 3: block 2 / 3), the running
+  // y of the previous / this block in fl (two alternating 64 x NR buffers), z_{c-1} in fl + 2 * 64 * NR
+  const bool fwd = fw.Y != nullptr;
+  const int yb0 = w == 1 ? 0 : w, ynb = w == 1 ? 2 : 1;
+  double yold[2][2];
+  double* yprev = fl + ((c + 1) & 1) * NB * GPX_MAX_RHS;
+  double* ycur = fl + (c & 1) * NB * GPX_MAX_RHS;
+  double* zp = fl + 2 * NB * GPX_MAX_RHS;
   if (c > 0) {
+    if (fwd && w > 0) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        if (b >= ynb) break;
+        const int row = c * NB + 16 * (yb0 + b) + (lane >> 2);
+        if (fw.nr == 1)
+          load_y<1>(fw, row, c == 1, yold[b]);
+        else
+          load_y<GPX_MAX_RHS>(fw, row, c == 1, yold[b]);
+      }
+    }
+    if (fwd && w >= 2) {
+      // z_{c-1} = D_{c-1} y_{c-1} (before chol16 overwrites sX: counted in srow below)
+      for (int rb = 2 * (w - 2); rb < 2 * (w - 2) + 2; ++rb) {
+        if (fw.nr == 1)
+          z_rows16<1>(fw, sX, yprev, c - 1, rb, zp);
+        else
+          z_rows16<GPX_MAX_RHS>(fw, sX, yprev, c - 1, rb, zp);
+      }
+      lds_add(&sh.zcnt);
+    }
     if (w > 0) {
       // the previous step's L_{c-1,c-1} (in sN) and D_{c-1} (in sX) leave while wave 0 starts this step; the last of
       // waves 1-3 to drain them publishes chain word 2c (D_{c-1} readable: the stage c-1 tasks of the pool start)
@@ -378,8 +538,9 @@ __device__ __forceinline__ int chain_step(const Sync& s, int c, int nblk, double
                  Dinv + (int64_t)(c - 1) * NB * NB, W, ldw, c - 1, w);
     }
     d4 acc[4];
+    double* Lrow = A + (int64_t)c * NB * lda + (int64_t)(c - 1) * NB;
     rowblock_times_lower_t(acc, sB, sX, w);  // reads only this wave's rows of sB
-    rowblock_out(acc, w, A + (int64_t)c * NB * lda + (int64_t)(c - 1) * NB, lda, sB);
+    rowblock_out(acc, w, w ? Lrow : nullptr, lda, sB);  // wave 0's rows leave through waves 1-3 below
     GPX_DAG_STAMP(0, c, 0, 1);
     lds_add(&sh.srow);
     if (w == 0) {
@@ -389,13 +550,28 @@ __device__ __forceinline__ int chain_step(const Sync& s, int c, int nblk, double
       lds_wait(&sh.srow, 4);  // every wave's S reads of D_{c-1} (and stores of it) are done before chol16 overwrites sX
       GPX_DAG_STAMP(0, c, 0, 2);
     } else {
+      // L_{c,c-1} and D_{c-1} leave before the factorisation starts: the last of waves 1-3 to drain publishes chain
+      // word 2c+1 (the pool's stage c-1 tasks and the critical task's column c both start from it)
+      lds_wait(&sh.srow, 4);
+      rows16_out(sB, Lrow, lda);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lds_add(&sh.pub) == 2 && lane == 0)
-        __hip_atomic_store(s.chain(), 2 * c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      lds_wait(&sh.srow, 4);
+        __hip_atomic_store(s.chain(), 2 * c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (w == 1) syrk3<1, 0, 2, 1, 3, 1>(sA, sB);
       else if (w == 2) syrk3<1, 1, 2, 2, 3, 2>(sA, sB);
       else syrk3<2, 0, 3, 0, 3, 3>(sA, sB);
+      if (fwd) {  // y_c -= L_{c,c-1} z_{c-1} into LDS (z_c = D_c y_c leaves in the next step)
+        lds_wait(&sh.zcnt, 2);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          if (b >= ynb) break;
+          const int rb = yb0 + b;
+          if (fw.nr == 1)
+            fwd_rows16<1>(fw, sB + 16 * rb * LD, zp, yold[b], 0, ycur, 16 * rb);
+          else
+            fwd_rows16<GPX_MAX_RHS>(fw, sB + 16 * rb * LD, zp, yold[b], 0, ycur, 16 * rb);
+        }
+      }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // L_{c,c-1} drained before the first barrier (published after it)
   }
@@ -408,8 +584,6 @@ __device__ __forceinline__ int chain_step(const Sync& s, int c, int nblk, double
     }
     __syncthreads();  // L_qq, D_qq (q = 0: also A_cc -= L L^T and the stores of L_{c,c-1})
     GPX_DAG_STAMP(0, c, 0, 3 + q);
-    if (q == 0 && c > 0 && t == 64)
-      __hip_atomic_store(s.chain(), 2 * c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (w == 0) {
       if (q < 3) tsolve(q + 1, q);
       lds_add(&sh.cnt);
@@ -437,7 +611,7 @@ __device__ __forceinline__ int chain_step(const Sync& s, int c, int nblk, double
       } else if (q == 3) {
         xfinish(3, w - 1, ptail);
       }
-      if (q == 1 || q == 2) try_prefetch();
+      if (q >= 1) try_prefetch();
     }
   }
   if (t == 0) sh.fail = fail;
@@ -522,10 +696,11 @@ struct Args {
   int lend[3];
   int wend[2];  // workers: blockIdx.x in [1, wend[0]) critical, [wend[0], wend[1]) front, the rest bulk
   unsigned spin_limit;
+  Fwd fw;  // forward substitution (fw.Y == nullptr: none)
 };
 
 __device__ void chain_role(const Args& g, double* A, double* Dinv, double* W, int32_t* info, const Sync& s,
-                           double* lds) {
+                           double* lds, const Fwd& fw, double* fl) {
   double* sA = lds;
   double* sB = lds + TILE_D;
   double* sX = lds + 2 * TILE_D;
@@ -536,10 +711,12 @@ __device__ void chain_role(const Args& g, double* A, double* Dinv, double* W, in
   const int nblk = g.nblk;
   auto blk = [&](int i, int j) { return A + (int64_t)i * NB * lda + (int64_t)j * NB; };
   tile_in(blk(0, 0), lda, sA);
+  if (fw.Y)  // y_0 = b_0
+    for (int e = t; e < NB * fw.nr; e += WG) fl[e] = rhs_b(fw, e / fw.nr, e % fw.nr);
   __syncthreads();
   for (int c = 0; c < nblk; ++c) {
     GPX_DAG_STAMP(0, c, 0, 0);
-    const int f = chain_step(s, c, nblk, A, lda, Dinv, W, g.ldw, sA, sB, sX, sN, sh);
+    const int f = chain_step(s, c, nblk, A, lda, Dinv, W, g.ldw, sA, sB, sX, sN, sh, fw, fl);
     if (f >= 0) {
       if (t == 0) {
         atomicCAS(info, 0, c * NB + f + 1);
@@ -548,6 +725,15 @@ __device__ void chain_role(const Args& g, double* A, double* Dinv, double* W, in
       break;
     }
     if (c + 1 == nblk) {  // the last factor and inverse (earlier ones leave during the next step)
+      if (fw.Y && (t >> 6) >= 2) {  // and the last z
+        const int w = t >> 6;
+        for (int rb = 2 * (w - 2); rb < 2 * (w - 2) + 2; ++rb) {
+          if (fw.nr == 1)
+            z_rows16<1>(fw, sX, fl + (c & 1) * NB * GPX_MAX_RHS, c, rb, nullptr);
+          else
+            z_rows16<GPX_MAX_RHS>(fw, sX, fl + (c & 1) * NB * GPX_MAX_RHS, c, rb, nullptr);
+        }
+      }
       tile_out<true>(sA, blk(c, c), lda);
       tile_out<true>(sX, Dinv + (int64_t)c * NB * NB, NB);
       if (W) {
@@ -581,13 +767,63 @@ __device__ void chain_role(const Args& g, double* A, double* Dinv, double* W, in
   }
 }
 
-// The front columns of stage k: k+1 and k+2, and k+3 when k is even (column k+3 odd: its 128-column pair leaves the
-// bulk tiles one stage before its first column does).  Every other (column, stage) update is a bulk U128 tile.
-__host__ __device__ inline int front_cols(int k, int nblk, int (&cols)[3]) {
+// The front columns of stage k: k+1, k+2, k+3, and k+4 when k is odd, so that the 128-column pair J = {2J, 2J+1} leaves
+// the bulk tiles after stage 2J-4 and its stages 2J-3 .. 2J-1 (2J) are FR column updates - among them the diagonal
+// blocks' stage 2J-3, which the critical task FR(2J, 2J-2) would otherwise wait for at the end of a 128x128 bulk tile.
+constexpr int kMaxFront = 4;
+__host__ __device__ inline int front_cols(int k, int nblk, int (&cols)[kMaxFront]) {
   int n = 0;
-  for (int j = k + 1; j <= k + 3 && j < nblk; ++j)
-    if (j < k + 3 || !(k & 1)) cols[n++] = j;
+  for (int j = k + 1; j <= k + 4 && j < nblk; ++j)
+    if (j < k + 4 || (k & 1)) cols[n++] = j;
   return n;
+}
+
+// The first stage a bulk tile of column pair J no longer receives.
+__host__ __device__ inline int bulk_limit(int J) { return 2 * J - 3; }
+
+// The order in which FR(i, k) updates its front blocks (j <= i): the critical task FR(k+2, k) the diagonal block and
+// then column k+1; the others column k+1 (L_{k+1,k} comes first, from the chain), the diagonal block, the rest.
+__host__ __device__ inline int fr_order(int i, int k, int nblk, int (&order)[kMaxFront]) {
+  int cols[kMaxFront];
+  const int nc = front_cols(k, nblk, cols);
+  int n = 0;
+  if (i == k + 2) {
+    order[n++] = k + 2;
+    order[n++] = k + 1;
+    return n;
+  }
+  for (int q = 0; q < nc; ++q)
+    if (cols[q] == k + 1 && cols[q] < i) order[n++] = cols[q];
+  for (int q = 0; q < nc; ++q)
+    if (cols[q] == i) order[n++] = cols[q];
+  for (int q = 0; q < nc; ++q)
+    if (cols[q] != k + 1 && cols[q] < i) order[n++] = cols[q];
+  return n;
+}
+
+// FR's stage of the forward substitution: z_k into LDS and the lane's y values of row block i (after the wait for D_k,
+// which z_k travels with), then y_i -= L_ik z_k on the wave's rows into yb, before FR publishes L_ik.
+__device__ __forceinline__ void fr_forward_load(const Fwd& fw, int i, int k, double (&yo)[2], double* zs) {
+  if (!fw.Y) return;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int row = i * NB + 16 * w + (lane >> 2);
+  if (fw.nr == 1)
+    load_y<1>(fw, row, k == 0, yo);
+  else
+    load_y<GPX_MAX_RHS>(fw, row, k == 0, yo);
+  const rsrc_t r = rsrc(fw.zbuf() + (int64_t)k * NB * fw.nr);
+  for (int e = t; e < NB * fw.nr; e += WG) zs[e] = ld1(r, e * 8);
+}
+
+__device__ __forceinline__ void fr_forward_apply(const Fwd& fw, int i, const double* sL, const double* zs,
+                                                 double (&yo)[2]) {
+  if (!fw.Y) return;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int row = i * NB + 16 * w + (lane >> 2);
+  if (fw.nr == 1)
+    fwd_rows16<1>(fw, sL + 16 * w * LD, zs, yo, row, nullptr, 0);
+  else
+    fwd_rows16<GPX_MAX_RHS>(fw, sL + 16 * w * LD, zs, yo, row, nullptr, 0);
 }
 
 // FR(i, k): L_ik = A_ik D_k^T (published as soon as it is stored), then row i of stage k on the front columns j <= i:
@@ -595,39 +831,36 @@ __host__ __device__ inline int front_cols(int k, int nblk, int (&cols)[3]) {
 // with L_{k+1,k} from the chain and L_{k+2,k} / L_{k+3,k} from FR(k+2, k) / FR(k+3, k).  One task per row and stage
 // (L_ik stays in LDS for every product), so the chain's next tiles (c+1, c) and (c+1, c+1) come from ONE task,
 // FR(c+1, c-1): one hand-off on the cycle chain -> pool -> chain.
-__device__ bool task_fr(const Args& g, double* A, double* Dinv, const Sync& s, int i, int k, double* lds, int idx) {
+__device__ bool task_fr(const Args& g, double* A, double* Dinv, const Sync& s, int i, int k, double* lds, int idx,
+                        const Fwd& fw, double* zs) {
   double* sA = lds;
   double* sB = lds + TILE_D;
   double* sX = lds + 2 * TILE_D;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int64_t lda = g.lda;
   auto blk = [&](int a, int b) { return A + (int64_t)a * NB * lda + (int64_t)b * NB; };
-  int cols[3];
-  const int ncol = front_cols(k, g.nblk, cols);
   {
     // lane 0: D_k published; lane 1: A_ik final through column k-1 (the front blocks are waited for one by one below)
     const int* mine = lane == 0 ? s.chain() : (lane == 1 ? s.ver(i, k) : nullptr);
     if (!wg_wait(s, mine, lane == 0 ? 2 * k + 2 : k, g.spin_limit)) return false;
   }
   GPX_DAG_TASK_STAMP(idx, 2);
+  double yo[2];
+  fr_forward_load(fw, i, k, yo, zs);
   tile_in(blk(i, k), lda, sA);
   tile_in(Dinv + (int64_t)k * NB * NB, NB, sX);
   __syncthreads();
   d4 acc[4];
   rowblock_times_lower_t(acc, sA, sX, w);
   rowblock_out(acc, w, blk(i, k), lda, sA);
+  fr_forward_apply(fw, i, sA, zs, yo);
   wg_publish(t == 0 ? s.lrow(i) : nullptr, k + 1);
   GPX_DAG_TASK_STAMP(idx, 3);
   // front blocks in the order the chain needs them: column k+1 (the chain's next tile (k+2, k+1) when i = k+2), the
   // diagonal block, then the others.  Each waits for its own version (the bulk tile of a column pair entering the
   // front lands late in its stage) and, off the diagonal, for L_jk.
-  int order[3], nord = 0;
-  for (int q = 0; q < ncol; ++q)
-    if (cols[q] == k + 1 && cols[q] < i) order[nord++] = cols[q];
-  for (int q = 0; q < ncol; ++q)
-    if (cols[q] == i) order[nord++] = cols[q];
-  for (int q = 0; q < ncol; ++q)
-    if (cols[q] != k + 1 && cols[q] < i) order[nord++] = cols[q];
+  int order[kMaxFront];
+  const int nord = fr_order(i, k, g.nblk, order);
   for (int q = 0; q < nord; ++q) {
     const int j = order[q];
     {
@@ -650,6 +883,59 @@ __device__ bool task_fr(const Args& g, double* A, double* Dinv, const Sync& s, i
     }
     wg_publish(t == 0 ? s.ver(i, j) : nullptr, k + 1);
   }
+  GPX_DAG_TASK_STAMP(idx, 4);
+  return true;
+}
+
+// FR(k+2, k), the critical task (the chain's step k+2 starts from its two front blocks): the same arithmetic as task_fr,
+// with every operand that does not come from the chain loaded BEFORE the chain's hand-offs, so that only D_k and
+// L_{k+1,k} are on the cycle chain -> task -> chain.  A_ik (-> L_ik), A_ii and A_{i,k+1} stay in LDS; D_k and then
+// L_{k+1,k} take the fourth tile.  The diagonal block first (it needs nothing from the chain beyond D_k).
+__device__ bool task_fr_crit(const Args& g, double* A, double* Dinv, const Sync& s, int k, double* lds, int idx,
+                             const Fwd& fw, double* zs) {
+  double* sL = lds;               // A_ik -> L_ik
+  double* sC = lds + TILE_D;      // A_{i,k+1}
+  double* sD = lds + 2 * TILE_D;  // D_k, then L_{k+1,k}
+  double* sG = lds + 3 * TILE_D;  // A_ii
+  const int i = k + 2;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int64_t lda = g.lda;
+  auto blk = [&](int a, int b) { return A + (int64_t)a * NB * lda + (int64_t)b * NB; };
+  {
+    const int* mine = lane == 0 ? s.ver(i, k) : (lane == 1 ? s.ver(i, k + 1) : (lane == 2 ? s.ver(i, i) : nullptr));
+    if (!wg_wait(s, mine, k, g.spin_limit)) return false;
+  }
+  tile_in(blk(i, k), lda, sL);
+  tile_in(blk(i, k + 1), lda, sC);
+  tile_in(blk(i, i), lda, sG);
+  {
+    const int* mine = lane == 0 ? s.chain() : nullptr;
+    if (!wg_wait(s, mine, 2 * k + 2, g.spin_limit)) return false;
+  }
+  GPX_DAG_TASK_STAMP(idx, 2);
+  double yo[2];
+  fr_forward_load(fw, i, k, yo, zs);
+  tile_in(Dinv + (int64_t)k * NB * NB, NB, sD);
+  __syncthreads();
+  d4 acc[4];
+  rowblock_times_lower_t(acc, sL, sD, w);
+  rowblock_out(acc, w, blk(i, k), lda, sL);
+  fr_forward_apply(fw, i, sL, zs, yo);
+  wg_publish(t == 0 ? s.lrow(i) : nullptr, k + 1);
+  GPX_DAG_TASK_STAMP(idx, 3);
+  syrk_lower(sG, sL, w);
+  __syncthreads();
+  tile_out<true>(sG, blk(i, i), lda);
+  wg_publish(t == 0 ? s.ver(i, i) : nullptr, k + 1);
+  {
+    const int* mine = lane == 0 ? s.chain() : nullptr;
+    if (!wg_wait(s, mine, 2 * k + 3, g.spin_limit)) return false;
+  }
+  tile_in(blk(k + 1, k), lda, sD);
+  __syncthreads();
+  rowblock_sub_abt(acc, sC, sL, sD, w);
+  rowblock_out(acc, w, blk(i, k + 1), lda, nullptr);
+  wg_publish(t == 0 ? s.ver(i, k + 1) : nullptr, k + 1);
   GPX_DAG_TASK_STAMP(idx, 4);
   return true;
 }
@@ -691,7 +977,8 @@ __device__ bool task_update(const Args& g, double* A, const Sync& s, int i, int 
   return true;
 }
 
-__device__ void pool_role(const Args& g, double* A, double* Dinv, const Sync& s, double* lds) {
+__device__ void pool_role(const Args& g, double* A, double* Dinv, const Sync& s, double* lds, const Fwd& fw,
+                          double* zs) {
   __shared__ int s_ticket;
   // the critical and front workers take their own list, then join the bulk list
   int which = (int)blockIdx.x < g.wend[0] ? 0 : ((int)blockIdx.x < g.wend[1] ? 1 : 2);
@@ -713,7 +1000,7 @@ __device__ void pool_role(const Args& g, double* A, double* Dinv, const Sync& s,
     GPX_DAG_TASK_STAMP(idx, 0);
     bool ok;
     if (type == T_FR)
-      ok = task_fr(g, A, Dinv, s, a, b, lds, idx);
+      ok = a == b + 2 ? task_fr_crit(g, A, Dinv, s, b, lds, idx, fw, zs) : task_fr(g, A, Dinv, s, a, b, lds, idx, fw, zs);
     else if (type == T_U64)
       ok = task_update<64>(g, A, s, a, b, k0, k1, lds, idx);
     else
@@ -737,11 +1024,13 @@ __global__ void __launch_bounds__(WG, 1) potrf_dag_kernel(Args g) {
   double* W = g.W ? g.W + prob * g.sw : nullptr;
   int32_t* info = g.info + prob;
   const Sync s{g.sync + prob * g.ss, g.nblk};
+  const Fwd& fw = g.fw;
   __shared__ __attribute__((aligned(16))) double lds[LDS_DOUBLES];
+  __shared__ __attribute__((aligned(16))) double fl[3 * NB * GPX_MAX_RHS];  // forward substitution vectors
   if (blockIdx.x == 0)
-    chain_role(g, A, Dinv, W, info, s, lds);
+    chain_role(g, A, Dinv, W, info, s, lds, fw, fl);
   else
-    pool_role(g, A, Dinv, s, lds);
+    pool_role(g, A, Dinv, s, lds, fw, fl);
   // a timed-out wait leaves the abort word at 2: every workgroup that saw it reports the distinct failure code
   if (threadIdx.x == 0 && __hip_atomic_load(s.abort_word(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 2)
     atomicCAS(info, 0, (int32_t)GPX_INFO_TIMEOUT);
@@ -764,6 +1053,8 @@ struct Plan {
   unsigned long long* dev = nullptr;
   double sim_us = 0.0;
   std::vector<double> sim_chain;  // simulated start of each chain step (diagnostics)
+  std::vector<double> sim_crit;   // critical FR(k+2, k): taken, tiles final, L_ik published, done, then the
+                                  // times its three tiles became final (diagnostics)
   double sim_busy_front = 0.0, sim_busy_bulk = 0.0;  // worker-microseconds busy
 };
 
@@ -774,10 +1065,13 @@ static unsigned long long encode(int type, int a, int b, int k0, int k1) {
 
 struct SimCost {
   double chain = 16.0;    // one chain step
-  double chain_s = 5.0;   // step start -> L_{c,c-1} published
+  double chain_s = 3.0;   // step start -> L_{c,c-1} published
   double hop = 2.0;       // publish -> visible to a polling workgroup
   double fr_s = 5.0;      // FR: start -> L_ik published
   double fr_u = 3.0;      // FR: one front block (tile load + 64x64x64 product + store + publish)
+  double crit_pre = 3.0;  // critical FR: its three tiles loaded before the chain's hand-off
+  double crit_s = 3.5;    // critical FR: D_k visible -> L_ik published (D_k load, product, store)
+  double crit_u = 2.5;    // critical FR: one front block from LDS operands (+ the L_{k+1,k} load for the column)
   double u64(int K) const { return 4.0 + 2.0 * K; }
   double u128(int K) const { return 6.0 + 10.0 * K; }
 };
@@ -787,7 +1081,7 @@ static Plan simulate(int nblk, int P, int F) {
   const int kMinChunk = 4, kMaxChunk = 8;
   const double dt = 0.25, INF = 1e30;
   Plan plan;
-  const int CW = nblk >= 3 ? std::min(2, std::max(1, P - F - 1)) : 0;  // critical workers
+  const int CW = nblk >= 3 ? std::min(3, std::max(1, P - F - 1)) : 0;  // critical workers
   plan.crit_workers = CW;
   plan.front_workers = F;
   const int M = nblk / 2;
@@ -813,18 +1107,25 @@ static Plan simulate(int nblk, int P, int F) {
   plan.lend[1] = (int)plan.list.size();
   std::vector<FTask> lists[2] = {crit, front};
   size_t lnext[2] = {0, 0};
-  struct BTile { int I, J, v; bool busy; };
+  plan.sim_crit.assign(7 * crit.size(), -1.0);
+  // bulk units: the 128x128 tiles (I, J), I > J, and the three 64-blocks of each diagonal tile (J, J) - the diagonal
+  // blocks' last bulk stages gate the critical task two steps later, and a U64 lands in a fraction of a U128's time
+  struct BTile { int T, a, b, J, v; bool busy; };
   std::vector<BTile> tiles;
-  for (int J = 2; J < M; ++J)
-    for (int I = J; I < M; ++I) tiles.push_back({I, J, 0, false});
+  for (int J = 2; J < M; ++J) {
+    tiles.push_back({64, 2 * J, 2 * J, J, 0, false});
+    tiles.push_back({64, 2 * J + 1, 2 * J, J, 0, false});
+    tiles.push_back({64, 2 * J + 1, 2 * J + 1, J, 0, false});
+    for (int I = J + 1; I < M; ++I) tiles.push_back({128, I, J, J, 0, false});
+  }
   size_t bulk_left = tiles.size();
   int cstep = 0;
   double cfree = 0.0;
   // cls: 0 critical, 1 front, 2 bulk; held: the FR task the worker holds (index into lists[cls], -1: none); phase 0:
   // waiting to start, 1 + q: front block q of its order next; tcur: when the task's previous phase ends
-  struct Worker { double free; int held; int cls; int phase; double tcur; };
+  struct Worker { double free; int held; int cls; int phase; double tcur, pre; };
   std::vector<Worker> wk(P);
-  for (int p = 0; p < P; ++p) wk[p] = {0.0, -1, p < CW ? 0 : (p < CW + F ? 1 : 2), 0, 0.0};
+  for (int p = 0; p < P; ++p) wk[p] = {0.0, -1, p < CW ? 0 : (p < CW + F ? 1 : 2), 0, 0.0, -1.0};
   struct Ev { double t; int kind, a, b, v; };  // kind 0 chain word, 1 lrow, 2 version, 3 tile free
   std::vector<Ev> evs;
   auto front_ready = [&](const FTask& f, double now) {
@@ -872,6 +1173,8 @@ static Plan simulate(int nblk, int P, int F) {
         if (lnext[w.cls] < lists[w.cls].size()) {
           w.held = (int)lnext[w.cls]++;
           w.phase = 0;
+          w.pre = -1.0;
+          if (w.cls == 0) plan.sim_crit[7 * w.held] = now;
         } else {
           w.cls = 2;  // joins the bulk
         }
@@ -879,33 +1182,43 @@ static Plan simulate(int nblk, int P, int F) {
       if (w.held >= 0) {
         front_busy = true;
         const FTask& f = lists[w.cls][w.held];
+        const bool crit = f.i == f.k + 2;
         if (w.phase == 0) {
-          if (!front_ready(f, now)) continue;
-          w.tcur = now + cost.fr_s;
+          if (crit) {
+            // its three tiles first (from the moment they are final), then D_k
+            if (w.pre < 0.0) {
+              if (VT(f.i, f.k, f.k) > now || VT(f.i, f.k + 1, f.k) > now || VT(f.i, f.i, f.k) > now) continue;
+              w.pre = now + cost.crit_pre;
+              plan.sim_crit[7 * w.held + 1] = now;
+              plan.sim_crit[7 * w.held + 4] = VT(f.i, f.k, f.k);
+              plan.sim_crit[7 * w.held + 5] = VT(f.i, f.k + 1, f.k);
+              plan.sim_crit[7 * w.held + 6] = VT(f.i, f.i, f.k);
+            }
+            if (chainT[2 * f.k + 2] > now) continue;
+            w.tcur = std::max(w.pre, chainT[2 * f.k + 2]) + cost.crit_s;
+            plan.sim_crit[7 * w.held + 2] = w.tcur;
+          } else {
+            if (!front_ready(f, now)) continue;
+            w.tcur = now + cost.fr_s;
+          }
           evs.push_back({w.tcur + cost.hop, 1, f.i, 0, f.k + 1});
           w.phase = 1;
         }
-        // column k+1, the diagonal block, then the other front columns, each once its version (and L block) is
-        // known; the task holds the worker meanwhile, as on the device
-        int cols[3];
-        const int nc = front_cols(f.k, nblk, cols);
-        int order[3], nord = 0;
-        for (int q = 0; q < nc; ++q)
-          if (cols[q] == f.k + 1 && cols[q] < f.i) order[nord++] = cols[q];
-        for (int q = 0; q < nc; ++q)
-          if (cols[q] == f.i) order[nord++] = cols[q];
-        for (int q = 0; q < nc; ++q)
-          if (cols[q] != f.k + 1 && cols[q] < f.i) order[nord++] = cols[q];
+        // the front blocks in fr_order, each once its version (and L block) is known; the task holds the worker
+        // meanwhile, as on the device
+        int order[kMaxFront];
+        const int nord = fr_order(f.i, f.k, nblk, order);
         while (w.phase - 1 < nord) {
           const int j = order[w.phase - 1];
-          double ready = VT(f.i, j, f.k);
+          double ready = crit ? 0.0 : VT(f.i, j, f.k);
           if (j != f.i) ready = std::max(ready, j == f.k + 1 ? chainT[2 * f.k + 3] : LT(j, f.k + 1));
           if (ready > now) break;  // not visible yet (or not even scheduled)
-          w.tcur = std::max(w.tcur, ready) + cost.fr_u;
+          w.tcur = std::max(w.tcur, ready) + (crit ? cost.crit_u : cost.fr_u);
           evs.push_back({w.tcur + cost.hop, 2, f.i, j, f.k + 1});
           ++w.phase;
         }
         if (w.phase - 1 < nord) continue;
+        if (crit && w.cls == 0) plan.sim_crit[7 * w.held + 3] = w.tcur;
         w.free = w.tcur;
         w.held = -1;
         continue;
@@ -918,10 +1231,12 @@ static Plan simulate(int nblk, int P, int F) {
     std::vector<Cand> cands;
     for (size_t q = 0; q < tiles.size(); ++q) {
       const BTile& b = tiles[q];
-      const int limit = 2 * b.J - 2;
+      const int limit = bulk_limit(b.J);
       if (b.busy || b.v >= limit) continue;
       int rel = limit;
-      for (int r : {2 * b.I, 2 * b.I + 1, 2 * b.J, 2 * b.J + 1}) {
+      int rows[4] = {b.a, b.b, b.a, b.b};
+      if (b.T == 128) rows[0] = 2 * b.a, rows[1] = 2 * b.a + 1, rows[2] = 2 * b.b, rows[3] = 2 * b.b + 1;
+      for (int r : rows) {
         int v = b.v;
         while (v < rel && LT(r, v + 1) <= now) ++v;
         rel = std::min(rel, v);
@@ -930,7 +1245,8 @@ static Plan simulate(int nblk, int P, int F) {
       if (avail <= 0) continue;
       const double deadline = cfree + (double)(limit - cstep) * cost.chain;
       const int remaining = limit - b.v;
-      const double rem_t = std::ceil((double)remaining / kMaxChunk) * cost.u128(std::min(remaining, kMaxChunk));
+      const int kc = std::min(remaining, kMaxChunk);
+      const double rem_t = std::ceil((double)remaining / kMaxChunk) * (b.T == 128 ? cost.u128(kc) : cost.u64(kc));
       const double slack = deadline - now - rem_t;
       if (avail < kMinChunk && rel < limit && slack > 2 * cost.chain) continue;
       cands.push_back({slack, (int)q, std::min(avail, kMaxChunk)});
@@ -943,15 +1259,18 @@ static Plan simulate(int nblk, int P, int F) {
       if (ni >= idle.size()) break;
       Worker& w = wk[idle[ni++]];
       BTile& b = tiles[cd.q];
-      plan.list.push_back(encode(T_U128, b.I, b.J, b.v, b.v + cd.K));
-      const double end = now + cost.u128(cd.K);
+      plan.list.push_back(encode(b.T == 128 ? T_U128 : T_U64, b.a, b.b, b.v, b.v + cd.K));
+      const double end = now + (b.T == 128 ? cost.u128(cd.K) : cost.u64(cd.K));
       b.v += cd.K;
-      for (int bi : {2 * b.I, 2 * b.I + 1})
-        for (int bj : {2 * b.J, 2 * b.J + 1})
-          if (bi >= bj) evs.push_back({end + cost.hop, 2, bi, bj, b.v});
+      if (b.T == 128) {
+        for (int bi : {2 * b.a, 2 * b.a + 1})
+          for (int bj : {2 * b.b, 2 * b.b + 1}) evs.push_back({end + cost.hop, 2, bi, bj, b.v});
+      } else {
+        evs.push_back({end + cost.hop, 2, b.a, b.b, b.v});
+      }
       b.busy = true;
       evs.push_back({end, 3, cd.q, 0, 0});
-      if (b.v >= 2 * b.J - 2) --bulk_left;
+      if (b.v >= bulk_limit(b.J)) --bulk_left;
       w.free = end;
     }
   }
@@ -1010,7 +1329,7 @@ int potrf_dag_workers(Context* c, int npad, int batch) {
 }
 
 hipError_t launch_potrf_dag(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info,
-                            const Batch& bt, double* W, int64_t ldw) {
+                            const Batch& bt, double* W, int64_t ldw, const ForwardRhs* fr) {
   const int nblk = npad / NB;
   const int G = potrf_dag_workers(c, npad, bt.count);
   if (!G) return hipErrorInvalidValue;
@@ -1062,6 +1381,12 @@ hipError_t launch_potrf_dag(Context* c, int npad, double* A, int64_t lda, double
   g.wend[0] = 1 + plan.crit_workers;
   g.wend[1] = 1 + plan.crit_workers + plan.front_workers;
   g.spin_limit = c->spin_limit;
+  g.fw = dag::Fwd{nullptr, 0, 0, 0, 0, 0, 1, 0.0, nullptr, nullptr};
+  if (fr && fr->Y) {
+    const int nr = rhs_row(fr->nrhs);
+    g.fw = dag::Fwd{fr->Y, fr->ldy, fr->sy, 2 * (int64_t)npad * nr, fr->nrhs, fr->n, nr, fr->mean, fr->buf,
+                    fr->buf + (int64_t)npad * nr};
+  }
   dag::potrf_dag_kernel<<<dim3(G, bt.count), WG, 0, c->stream>>>(g);
   return hipGetLastError();
 }

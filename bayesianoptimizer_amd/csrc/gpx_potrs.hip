@@ -325,13 +325,14 @@ __device__ __forceinline__ void fma_bwd(double (&acc)[4][NR], const TileRegs& R,
 __device__ void potrs_items_1(int n, int npad, const double* __restrict__ L, int64_t ldl,
                               const double* __restrict__ Dinv, const double* __restrict__ Y, int64_t ldy,
                               double const_mean, double* __restrict__ alpha, gu64* gz, gu64* ga, gu32* abort_word,
-                              unsigned limit, SolveLds1& s, int& s_abort) {
+                              unsigned limit, SolveLds1& s, int& s_abort, const double* __restrict__ zin) {
   const int t = threadIdx.x, w = t >> 6;
   const int nb = npad / SB;
   const int G = gridDim.x;
   // blocks g, g + G, ... of this workgroup: forward ascending, then backward descending (see the file comment)
   const int nown = (nb - (int)blockIdx.x + G - 1) / G;
-  for (int step = 0; step < 2 * nown; ++step) {
+  // zin: z from the factorisation, backward items only
+  for (int step = zin ? nown : 0; step < 2 * nown; ++step) {
     const bool fwd = step < nown;
     const int K = (int)blockIdx.x + (fwd ? step : 2 * nown - 1 - step) * G;
     const int64_t r0 = (int64_t)K * SB;
@@ -347,9 +348,11 @@ __device__ void potrs_items_1(int n, int npad, const double* __restrict__ L, int
     };
     if (jcount > 0) load_tile(ta, 0);  // in flight while D_KK is formed
     // the first backward item is the block of the last forward item: its D_KK is still in LDS
-    if (fwd || step != nown) form_block_inverse(s, Dinv, L, ldl, K);
+    if (fwd || step != nown || zin) form_block_inverse(s, Dinv, L, ldl, K);
     if (fwd) {
       if (t < SB) s.vs[t] = (r0 + t < n) ? Y[(r0 + t) * ldy] - const_mean : 0.0;
+    } else if (zin) {
+      if (t < SB) s.vs[t] = zin[r0 + t];
     } else if (w == 0) {
       if (!sweep_block<1>(gz + r0 * 2, 1u, s.vs, abort_word, limit) && (t & 63) == 0) s_abort = 1;
     }
@@ -471,14 +474,14 @@ template <int NR>
 __device__ void potrs_items(int n, int npad, const double* __restrict__ L, int64_t ldl, const double* __restrict__ Dinv,
                             const double* __restrict__ Y, int64_t ldy, int nrhs, double const_mean,
                             double* __restrict__ alpha, gu64* gz, gu64* ga, gu32* abort_word, unsigned limit,
-                            SolveLds<NR>& s, int& s_abort) {
+                            SolveLds<NR>& s, int& s_abort, const double* __restrict__ zin) {
   const int t = threadIdx.x, w = t >> 6;
   double* zw = s.zw[w];
   const int nb = npad / SB;
   const int G = gridDim.x;
   // blocks g, g + G, ... of this workgroup: forward ascending, then backward descending (see the file comment)
   const int nown = (nb - (int)blockIdx.x + G - 1) / G;
-  for (int step = 0; step < 2 * nown; ++step) {
+  for (int step = zin ? nown : 0; step < 2 * nown; ++step) {
     const bool fwd = step < nown;
     const int K = (int)blockIdx.x + (fwd ? step : 2 * nown - 1 - step) * G;
     const int64_t r0 = (int64_t)K * SB;
@@ -493,7 +496,7 @@ __device__ void potrs_items(int n, int npad, const double* __restrict__ L, int64
     };
     if (jcount > 0) load_tile(ta, 0);
     // diagonal 128-block: D_a, D_b (potrf's inverses of the 64-blocks) and L_ba
-    if (fwd || step != nown) {  // the first backward item reuses the last forward item's diagonal block
+    if (fwd || step != nown || zin) {  // the first backward item reuses the last forward item's diagonal block
       tile_to_lds(Dinv + (int64_t)(2 * K) * NB * NB, NB, s.Da);
       tile_to_lds(Dinv + (int64_t)(2 * K + 1) * NB * NB, NB, s.Db);
       tile_to_lds(L + (r0 + NB) * ldl + r0, ldl, s.Lba);
@@ -504,6 +507,8 @@ __device__ void potrs_items(int n, int npad, const double* __restrict__ L, int64
         const int64_t gi = r0 + row;
         s.vs[e] = (rr < nrhs && gi < n) ? Y[gi * ldy + rr] - const_mean : 0.0;
       }
+    } else if (zin) {
+      for (int e = t; e < SB * NR; e += WG) s.vs[e] = zin[r0 * NR + e];
     } else if (w == 0) {
       if (!sweep_block<NR>(gz + r0 * NR * 2, 1u, s.vs, abort_word, limit) && (t & 63) == 0) s_abort = 1;
     }
@@ -584,8 +589,10 @@ __global__ void __launch_bounds__(WG) potrs_kernel(int n, int npad, const double
                                                    int64_t ldy, int nrhs, double const_mean, double* __restrict__ alpha,
                                                    int32_t* __restrict__ info, unsigned long long* granules,
                                                    unsigned* abort_ptr, int64_t sl, int64_t sd, int64_t sy, int64_t sa,
-                                                   int64_t sg, unsigned limit) {
+                                                   int64_t sg, unsigned limit, const double* __restrict__ zin,
+                                                   int64_t sz) {
   const int prob = blockIdx.y;
+  if (zin) zin += prob * sz;
   L += prob * sl;
   Dinv += prob * sd;
   Y += prob * sy;
@@ -599,11 +606,12 @@ __global__ void __launch_bounds__(WG) potrs_kernel(int n, int npad, const double
   if constexpr (NR == 1) {
     __shared__ __attribute__((aligned(16))) SolveLds1 s;
     __syncthreads();
-    potrs_items_1(n, npad, L, ldl, Dinv, Y, ldy, const_mean, alpha, gz, ga, abort_word, limit, s, s_abort);
+    potrs_items_1(n, npad, L, ldl, Dinv, Y, ldy, const_mean, alpha, gz, ga, abort_word, limit, s, s_abort, zin);
   } else {
     __shared__ __attribute__((aligned(16))) SolveLds<NR> s;
     __syncthreads();
-    potrs_items<NR>(n, npad, L, ldl, Dinv, Y, ldy, nrhs, const_mean, alpha, gz, ga, abort_word, limit, s, s_abort);
+    potrs_items<NR>(n, npad, L, ldl, Dinv, Y, ldy, nrhs, const_mean, alpha, gz, ga, abort_word, limit, s, s_abort,
+                    zin);
   }
   // a timed-out hand-off: alpha holds NaN; the problem's pivot word reports it (GPX_INFO_TIMEOUT), so a caller that
   // checks info never mistakes the NaN scores for a result
@@ -622,7 +630,7 @@ size_t potrs_clear_bytes(int64_t npad, int64_t nrhs, int64_t batch) {
 
 hipError_t launch_potrs(Context* c, int n, int npad, const double* L, int64_t ldl, const double* Dinv,
                         const double* Y, int64_t ldy, int nrhs, double const_mean, double* alpha,
-                        int32_t* info, void* ws, const Batch& bt, bool ws_cleared) {
+                        int32_t* info, void* ws, const Batch& bt, bool ws_cleared, const double* z, int64_t sz) {
   LaunchTimer tm(c, GPX_TIMER_ALPHA);
   const int nb = npad / SB;
   // granules of every problem, then one abort word per problem; zeroed as ONE block from the workspace start (by the
@@ -649,16 +657,21 @@ hipError_t launch_potrs(Context* c, int n, int npad, const double* L, int64_t ld
   if (nrhs == 1)
     potrs_kernel<1><<<dim3(G, bt.count), WG, 0, c->stream>>>(n, npad, L, ldl, Dinv, Y, ldy, nrhs, const_mean, alpha,
                                                              info, granules, abort_word, bt.k, bt.dinv, bt.y,
-                                                             bt.alpha, sg, c->spin_limit);
+                                                             bt.alpha, sg, c->spin_limit, z, sz);
   else
     potrs_kernel<GPX_MAX_RHS><<<dim3(G, bt.count), WG, 0, c->stream>>>(n, npad, L, ldl, Dinv, Y, ldy, nrhs,
                                                                        const_mean, alpha, info, granules, abort_word,
-                                                                       bt.k, bt.dinv, bt.y, bt.alpha, sg, c->spin_limit);
+                                                                       bt.k, bt.dinv, bt.y, bt.alpha, sg, c->spin_limit,
+                                                                       z, sz);
   return hipGetLastError();
 }
 
+size_t potrs_forward_offset(int64_t npad, int64_t nrhs, int64_t batch) {
+  return (potrs_clear_bytes(npad, nrhs, batch) + 255) & ~(size_t)255;
+}
+
 size_t potrs_workspace_bytes(int64_t npad, int64_t nrhs, int64_t batch) {
-  return potrs_clear_bytes(npad, nrhs, batch) + 64;
+  return potrs_forward_offset(npad, nrhs, batch) + (size_t)(2 * npad * rhs_row((int)nrhs)) * 8 * batch + 64;
 }
 
 }  // namespace gpx

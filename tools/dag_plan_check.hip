@@ -61,17 +61,12 @@ static bool check(int nblk, int P, bool verbose) {
       bool done = false;
       if (type == T_FR) {
         const int i = a, k = b;
-        int cols[3];
-        const int nc = front_cols(k, nblk, cols);
-        int order[3], nord = 0;
-        for (int c2 = 0; c2 < nc; ++c2)
-          if (cols[c2] == k + 1 && cols[c2] < i) order[nord++] = cols[c2];
-        for (int c2 = 0; c2 < nc; ++c2)
-          if (cols[c2] == i) order[nord++] = cols[c2];
-        for (int c2 = 0; c2 < nc; ++c2)
-          if (cols[c2] != k + 1 && cols[c2] < i) order[nord++] = cols[c2];
+        int order[kMaxFront];
+        const int nord = fr_order(i, k, nblk, order);
+        const bool crit = i == k + 2;
         if (state[q] == 1) {
-          if (chain >= 2 * k + 2 && ver[i * nblk + k] >= k) {
+          const bool pre = !crit || (ver[i * nblk + k + 1] >= k && ver[i * nblk + i] >= k);
+          if (chain >= 2 * k + 2 && ver[i * nblk + k] >= k && pre) {
             if (ver[i * nblk + k] != k) { printf("FR(%d,%d) tile version %d\n", i, k, ver[i * nblk + k]); return false; }
             lrow[i] = k + 1;
             ver[i * nblk + k] = k + 1;  // L final
@@ -140,7 +135,13 @@ int main() {
     printf("P=%d F=%d busy: front %.0f of %.0f, bulk %.0f of %.0f worker-us; chain starts:", P, pl.front_workers,
            pl.sim_busy_front, pl.front_workers * pl.sim_us, pl.sim_busy_bulk, (P - pl.front_workers) * pl.sim_us);
     for (size_t c = 0; c < pl.sim_chain.size(); c += 4) printf(" %.0f", pl.sim_chain[c]);
-    printf("\n");
+    printf("\n  critical FR(c+1,c-1) relative to chain step c start: taken, tiles final, L published, done | next step\n");
+    for (size_t c = 2; c + 1 < pl.sim_chain.size(); c += (P == 255 ? 1 : 5)) {
+      const double b = pl.sim_chain[c];
+      const double* x = &pl.sim_crit[7 * (c - 1)];
+      printf("  c=%2zu %7.1f %7.1f %7.1f %7.1f | %7.1f   tiles (c+1,c-1) %6.1f (c+1,c) %6.1f (c+1,c+1) %6.1f\n", c,
+             x[0] - b, x[1] - b, x[2] - b, x[3] - b, pl.sim_chain[c + 1] - b, x[4] - b, x[5] - b, x[6] - b);
+    }
   }
   printf("%s\n", ok ? "PLAN CHECK OK" : "PLAN CHECK FAILED");
   return ok ? 0 : 1;

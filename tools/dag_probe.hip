@@ -249,6 +249,55 @@ int main(int argc, char** argv) {
     printf("batched x%d: best %.3f ms, info %d %d.., lower entries differing from single fits: %d\n", batch, ms, hi[0],
            batch > 1 ? hi[1] : 0, mism);
   }
+  // forward substitution folded into the factorisation: z = L^{-1} (Y - mean) against a host substitution with the
+  // device's own L (1 and 3 right-hand sides, n - 5 real rows so that the padding is exercised)
+  for (int nrhs : {1, 3}) {
+    const int nr = nrhs == 1 ? 1 : GPX_MAX_RHS;
+    const int nreal = n - 5;
+    const double mean = 0.25;
+    std::vector<double> Yh((size_t)nreal * nrhs);
+    for (size_t e = 0; e < Yh.size(); ++e) Yh[e] = std::sin(0.37 * (double)e) + 0.1 * (double)(e % 7);
+    double *Yd = nullptr, *fb = nullptr;
+    CK(hipMalloc(&Yd, Yh.size() * 8));
+    CK(hipMalloc(&fb, (size_t)2 * n * nr * 8));
+    CK(hipMemcpy(Yd, Yh.data(), Yh.size() * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(A, K.data(), bytes, hipMemcpyHostToDevice));
+    ForwardRhs fr;
+    fr.Y = Yd;
+    fr.ldy = nrhs;
+    fr.nrhs = nrhs;
+    fr.n = nreal;
+    fr.mean = mean;
+    fr.buf = fb;
+    bool zd = false;
+    ctx.potrf_schedule = 2;
+    CK(hipMemsetAsync(info, 0, 4, ctx.stream));
+    CK(launch_potrf(&ctx, n, A, n, D, info, one, nullptr, 0, &fr, &zd));
+    CK(hipStreamSynchronize(ctx.stream));
+    std::vector<double> Lz((size_t)n * n), zdev((size_t)n * nr);
+    CK(hipMemcpy(Lz.data(), A, bytes, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(zdev.data(), fb + (size_t)n * nr, zdev.size() * 8, hipMemcpyDeviceToHost));
+    double err = 0, zmax = 0;
+    long bad = 0;
+    for (int rr = 0; rr < nr; ++rr) {
+      std::vector<double> z(n);
+      for (int i = 0; i < n; ++i) {
+        double v = (i < nreal && rr < nrhs) ? Yh[(size_t)i * nrhs + rr] - mean : 0.0;
+        for (int k = 0; k < i; ++k) v -= Lz[(size_t)i * n + k] * z[k];
+        z[i] = v / Lz[(size_t)i * n + i];
+      }
+      for (int i = 0; i < n; ++i) {
+        const double dv = zdev[(size_t)i * nr + rr];
+        if (!std::isfinite(dv)) ++bad;
+        err = std::max(err, fabs(dv - z[i]));
+        zmax = std::max(zmax, fabs(z[i]));
+      }
+    }
+    printf("forward substitution nrhs=%d: z_done %d, max|z_dev - z_host| = %.3e (max|z| %.3e), non-finite %ld\n", nrhs,
+           (int)zd, err, zmax, bad);
+    CK(hipFree(Yd));
+    CK(hipFree(fb));
+  }
   // NOT_PD: a negative diagonal entry deep inside
   {
     std::vector<double> Kb = K;
