@@ -38,7 +38,7 @@ struct Context {
   // bounded spins of the in-launch hand-offs (potrf DAG, potrs): passes before a waiter gives up and reports a timeout
   unsigned spin_limit = 1u << 22;
   // options (include/gpx.h GPX_OPT_*; set by gpx_set_option or GPX_OPTIONS at gpx_create)
-  int potrf_schedule = 0;  // 0 by size (dataflow for npad <= 4096), 1 multi-launch, 2 dataflow where it applies
+  int potrf_schedule = 0;  // 0 by size (multi-launch: measured faster at every size), 1 multi-launch, 2 dataflow where it applies
   int sweep_fused = 1;     // fused small-n sweep where it applies
   int gram_split = 0;      // 0 by size, else workgroups per Gram tile
   int potrf_lazy = 0;      // multi-launch flush interval, 0 by size

@@ -50,8 +50,11 @@ using Tile128 = MfmaTile<2 * NB, 2 * NB, 16, false, false>;  // trailing update
 constexpr int LDD = 20;
 constexpr int DBUF = 768;  // >= 2 * 16 * LDD (+ 128 of chol16_mfma's factor tables), and sP + D buffers hold Tile64::LDS_DOUBLES
 static_assert(NB * LD64 + DBUF >= Tile64::LDS_DOUBLES && DBUF >= 2 * 16 * LDD + 128, "panel LDS aliasing");
-constexpr int PANEL_LDS = 2 * NB * LD64 + DBUF;
+// + the forward fold's right-hand sides of a p > 0 panel workgroup (64 x GPX_MAX_RHS, stored at the workgroup's end:
+// a global store before a barrier would hold the barrier until it completes)
+constexpr int PANEL_LDS = 2 * NB * LD64 + DBUF + NB * GPX_MAX_RHS;
 constexpr int STEP_LDS = PANEL_LDS > Tile128::LDS_DOUBLES ? PANEL_LDS : Tile128::LDS_DOUBLES;
+static_assert(STEP_LDS * 8 + 64 <= 81920, "two workgroups per CU");
 
 // C - L_a L_b^T for a 64x64 tile into the LDS tile S (row length LD64): acc seeded with -C (its loads issued with the
 // first k-tile's, no load round trip after the product), acc += L_a L_b^T over K, S = -acc.
@@ -86,15 +89,109 @@ __device__ __forceinline__ d4 mfma_sub(double a, double b, d4 c) {  // c - a b
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 1);
 }
 
-template <int W, bool PANEL>
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ rsrc_t buf_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void st2_sc1(rsrc_t r, int off, double a, double b) {  // 16-byte write-through store
+  const unsigned long long x = __double_as_longlong(a), y = __double_as_longlong(b);
+  const u32x4_t v = {(unsigned)x, (unsigned)(x >> 32), (unsigned)y, (unsigned)(y >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
+__device__ __forceinline__ double swap_adjacent_lanes(double v) {  // DPP quad_perm [1, 0, 3, 2]
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(u & 0xffffffffull), 0xB1, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), 0xB1, 0xf, 0xf, false);
+  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// The forward half of alpha's triangular solve folded into the factorisation (launch_potrf with a ForwardRhs, eager
+// schedules only): z = L^{-1} (Y - mean) for NR = 1 or GPX_MAX_RHS right-hand-side columns (padded rows and columns
+// >= nrhs are 0).  Row block i's running right-hand side r_i = (Y - mean)_i - sum_{k < c} L_ik z_k is kept by the panel
+// workgroup of row i: in launch c >= 1 it subtracts L_{i,c-1} z_{c-1} with the L_{i,c-1} its pre-update has in LDS
+// anyway, and the p = 0 workgroup (i = c) then forms z_c = L_cc^{-1} r_c block by block inside the factorisation
+// (z_s = D_s r_s, r_s' -= L_s's z_s for s' > s), on wave 3, the wave with the fewest U items there.  r lives in
+// global memory between launches (npad x NR), z is written once per block (npad x NR).
+struct PotrfFwd {
+  const double* Y = nullptr;
+  int64_t ldy = 0, sy = 0;  // sy: Y stride per problem
+  double* r = nullptr;      // running right-hand sides (null: no fold)
+  double* z = nullptr;
+  int64_t sb = 0;           // r / z stride per problem
+  int nrhs = 1, n = 0;
+  double mean = 0.0;
+};
+
+__device__ __forceinline__ double fwd_y(const PotrfFwd& f, int row, int rr) {
+  return (row < f.n && rr < f.nrhs) ? f.Y[(int64_t)row * f.ldy + rr] - f.mean : 0.0;
+}
+
+__device__ __forceinline__ double dbl_of(unsigned lo, unsigned hi) {
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+// (x_0 + x_2) + (x_1 + x_3) over the four 16-lane rows q of a wave, the same value in every row: gfx950's
+// v_permlane32_swap / v_permlane16_swap (VALU) instead of two ds_bpermute round trips.
+__device__ __forceinline__ double rowsum4(double x) {
+#ifdef GPX_FOLD_SHFL
+  x += __shfl_xor(x, 32);
+  return x + __shfl_xor(x, 16);
+#else
+  const unsigned long long u = __double_as_longlong(x);
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)u, (unsigned)u, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(u >> 32), (unsigned)(u >> 32), false, false);
+  const double y = dbl_of(lo[0], hi[0]) + dbl_of(lo[1], hi[1]);  // rows (0+2, 1+3, 0+2, 1+3)
+  const unsigned long long v = __double_as_longlong(y);
+  const auto lo2 = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+  const auto hi2 = __builtin_amdgcn_permlane16_swap((unsigned)(v >> 32), (unsigned)(v >> 32), false, false);
+  return dbl_of(lo2[0], hi2[0]) + dbl_of(lo2[1], hi2[1]);  // even row + odd row
+#endif
+}
+
+// One wave: out[rr] = sum_k M[a][k] v[k][rr] for the 16-row block M (LDS, row length ldm, KQ columns per lane
+// quarter: K = 4 KQ) and v (LDS, K x NR); lane = a + 16 kq sums its quarter, the quarters are combined by two
+// cross-lane exchanges in a fixed order, so every lane of row a holds the same total.
+template <int NR, int KQ>
+__device__ __forceinline__ void wave_matvec16(const double* M, int ldm, const double* v, double (&out)[NR]) {
+  const int lane = threadIdx.x & 63, a = lane & 15, kq = lane >> 4;
+#pragma unroll
+  for (int rr = 0; rr < NR; ++rr) out[rr] = 0.0;
+#pragma unroll
+  for (int k = 0; k < KQ; ++k) {
+    const int kk = kq * KQ + k;
+    const double m = M[a * ldm + kk];
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) out[rr] = fma(m, v[kk * NR + rr], out[rr]);
+  }
+#pragma unroll
+  for (int rr = 0; rr < NR; ++rr) out[rr] = rowsum4(out[rr]);
+}
+
+// LDS stores of one lane, then reads of them by other lanes of the same wave (LDS is in order per wave; this keeps
+// the compiler from moving the reads up)
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <int W, bool PANEL, int NR>
 __device__ __forceinline__ void update_eager_wave(const double* __restrict__ Acc, const double* __restrict__ Aic,
                                                   const double* __restrict__ Lc, const double* __restrict__ Li,
-                                                  int64_t lda, double* sA, double* sP, int c, int p) {
+                                                  int64_t lda, double* sA, double* sP, int c, int p,
+                                                  const PotrfFwd& f, double* sZ, double* sR) {
   constexpr int NCC = W < 2 ? 3 : 2;
   const int t = threadIdx.x, lane = t & 63;
   const int g = lane >> 4, cl = lane & 15;
   double2 rl[8], ri[8];
   d4 acc_cc[NCC], acc_ic[4];
+  // forward fold: z_{c-1} (-> LDS sZ) and this lane's old right-hand sides (row 16 W + cl of block c + p)
+  double2 zv = make_double2(0.0, 0.0);
+  double rold[NR > 0 ? NR : 1];
+  const int frow = (c + p) * NB + 16 * W + cl;
+  if constexpr (NR > 0) {
+    if (t < 32 * NR) zv = *reinterpret_cast<const double2*>(f.z + (int64_t)(c - 1) * NB * NR + 2 * t);
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr)
+      rold[rr] = g != 0 ? 0.0 : (c == 1 ? fwd_y(f, frow, rr) : f.r[(int64_t)frow * NR + rr]);
+  }
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int e = (t + q * WG) * 2, r = e >> 6, cc = e & 63;
@@ -119,12 +216,20 @@ __device__ __forceinline__ void update_eager_wave(const double* __restrict__ Acc
     *reinterpret_cast<double2*>(sA + r * LD64 + cc) = rl[q];
     if (PANEL) *reinterpret_cast<double2*>(sP + r * LD64 + cc) = ri[q];
   }
+  if constexpr (NR > 0) {
+    if (t < 32 * NR) *reinterpret_cast<double2*>(sZ + 2 * t) = zv;
+  }
   __syncthreads();
   GPX_EAGER_STAMP(c, p, 0);
   // k in chunks of 16: one batch of fragment reads (the four L_c row blocks serve as the B operand of every block and as
   // the A operand of the A_cc blocks; L_i's row block W is A_ic's A operand), then the chunk's MFMAs, independent
   // across blocks
   const int m = lane & 15, kq = lane >> 4;
+  // forward fold: r_i -= L_{i,c-1} z_{c-1} on the wave's 16 rows, from the L fragments the MFMAs read anyway (row block
+  // W of L_i, or of L_c for p = 0): lane (m, kq) sums k = kq mod 4, its FMAs issue between the chunk's MFMAs
+  double part[NR > 0 ? NR : 1];
+#pragma unroll
+  for (int rr = 0; rr < (NR > 0 ? NR : 1); ++rr) part[rr] = 0.0;
 #pragma unroll
   for (int kc = 0; kc < NB; kc += 16) {
     double fc[4][4], fi[4];
@@ -143,6 +248,21 @@ __device__ __forceinline__ void update_eager_wave(const double* __restrict__ Acc
 #pragma unroll
       for (int b = 0; b < NCC; ++b)
         acc_cc[b] = mfma_sub(fc[kLowerBlk[W + 4 * b][0]][s], fc[kLowerBlk[W + 4 * b][1]][s], acc_cc[b]);
+      if constexpr (NR > 0) {
+        const double lv = PANEL ? fi[s] : fc[W][s];
+#pragma unroll
+        for (int rr = 0; rr < NR; ++rr) part[rr] = fma(lv, sZ[(kc + 4 * s + kq) * NR + rr], part[rr]);
+      }
+    }
+  }
+  if constexpr (NR > 0) {
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) part[rr] = rowsum4(part[rr]);
+    if (g == 0) {
+#pragma unroll
+      for (int rr = 0; rr < NR; ++rr) {
+        sR[(16 * W + cl) * NR + rr] = rold[rr] - part[rr];  // stored to global memory at the workgroup's end
+      }
     }
   }
   __syncthreads();  // every wave's operand reads done: sA / sP take the results
@@ -155,15 +275,44 @@ __device__ __forceinline__ void update_eager_wave(const double* __restrict__ Acc
   }
 }
 
-template <bool PANEL>
+template <bool PANEL, int NR>
 __device__ __forceinline__ void update_eager(const double* __restrict__ Acc, const double* __restrict__ Aic,
                                              const double* __restrict__ Lc, const double* __restrict__ Li, int64_t lda,
-                                             double* sA, double* sP, int c, int p) {
+                                             double* sA, double* sP, int c, int p, const PotrfFwd& f, double* sZ,
+                                             double* sR) {
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {  // wave-uniform: compile-time block lists per wave
-    case 0: update_eager_wave<0, PANEL>(Acc, Aic, Lc, Li, lda, sA, sP, c, p); break;
-    case 1: update_eager_wave<1, PANEL>(Acc, Aic, Lc, Li, lda, sA, sP, c, p); break;
-    case 2: update_eager_wave<2, PANEL>(Acc, Aic, Lc, Li, lda, sA, sP, c, p); break;
-    default: update_eager_wave<3, PANEL>(Acc, Aic, Lc, Li, lda, sA, sP, c, p); break;
+    case 0: update_eager_wave<0, PANEL, NR>(Acc, Aic, Lc, Li, lda, sA, sP, c, p, f, sZ, sR); break;
+    case 1: update_eager_wave<1, PANEL, NR>(Acc, Aic, Lc, Li, lda, sA, sP, c, p, f, sZ, sR); break;
+    case 2: update_eager_wave<2, PANEL, NR>(Acc, Aic, Lc, Li, lda, sA, sP, c, p, f, sZ, sR); break;
+    default: update_eager_wave<3, PANEL, NR>(Acc, Aic, Lc, Li, lda, sA, sP, c, p, f, sZ, sR); break;
+  }
+}
+
+// Waves w = 1..3 of the p = 0 panel workgroup at pivot step s (D_s = L_ss^{-1} in D, L_s's for s' > s published in
+// sA): each forms z_s = D_s r_s (the same arithmetic in every wave; wave 1 keeps it in sZall), then wave w applies
+// r_{s+w} -= L_{s+w,s} z_s, so no wave carries more than two 16 x 16 products per step.
+template <int NR>
+__device__ __forceinline__ void fwd_pivot_step(int s, int w, const double* D, const double* sA, double* sR,
+                                               double* sZs, double* sZall) {
+  const int lane = threadIdx.x & 63, a = lane & 15, kq = lane >> 4;
+  double part[NR];
+  double* zw = sZs + (w - 1) * 16 * NR;  // this wave's copy of z_s
+  wave_matvec16<NR, 4>(D, LDD, sR + 16 * s * NR, part);
+  if (kq == 0) {
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) {
+      zw[a * NR + rr] = part[rr];
+      if (w == 1) sZall[(16 * s + a) * NR + rr] = part[rr];
+    }
+  }
+  const int s2 = s + w;
+  if (s2 < 4) {
+    wave_lds_sync();
+    wave_matvec16<NR, 4>(sA + 16 * s2 * LD64 + 16 * s, LD64, zw, part);
+    if (kq == 0) {
+#pragma unroll
+      for (int rr = 0; rr < NR; ++rr) sR[(16 * s2 + a) * NR + rr] -= part[rr];
+    }
   }
 }
 
@@ -178,9 +327,11 @@ __device__ __forceinline__ void load_tile_lds(const double* __restrict__ G, int6
   }
 }
 
-// Panel workgroup p of block column c (see the file comment).
+// Panel workgroup p of block column c (see the file comment); NR > 0: with the forward fold (PotrfFwd).
+template <int NR>
 __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, int c, int p, int nblk, int c0,
-                                           double* __restrict__ Dinv, int32_t* __restrict__ info, double* lds) {
+                                           double* __restrict__ Dinv, int32_t* __restrict__ info, double* lds,
+                                           const PotrfFwd& f) {
   double* sA = lds;             // A_cc -> L_cc
   double* sP = sA + NB * LD64;  // A_ic -> L_ic (p > 0)
   double* sDb = sP + NB * LD64; // D_ss, double-buffered by step parity (2 x 16 x LDD)
@@ -188,6 +339,13 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
   __shared__ int s_tdone;              // T items published (4 per step)
   const int t = threadIdx.x, w = t >> 6;
   const bool panel = p > 0;
+  // forward fold: z_{c-1} staged in the D buffers during the pre-update; r_i of a p > 0 workgroup in the area after the
+  // D buffers; for p = 0 (which never uses sP) r_c, z_s and z_c in sP
+  double* sZ = sDb;
+  double* sR = panel ? sDb + DBUF : sP;
+  double* sZall = sP + NB * GPX_MAX_RHS;
+  double* sZs = sZall + NB * GPX_MAX_RHS;  // one 16 x NR slot per wave 1..3
+  static_assert(NB * GPX_MAX_RHS <= DBUF && 2 * NB * GPX_MAX_RHS + 3 * 16 * GPX_MAX_RHS <= NB * LD64, "fold LDS");
   const int nrow = panel ? 8 : 4;  // 16-row blocks of the tall panel
   const int bi = c + p;
   const double* Acc = A + (int64_t)c * NB * lda + (int64_t)c * NB;
@@ -202,12 +360,13 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
 #ifndef GPX_POTRF_TILE_PREUPDATE
     if (kk == NB) {
       if (panel)
-        update_eager<true>(Acc, Aic, Lc, Li, lda, sA, sP, c, p);
+        update_eager<true, NR>(Acc, Aic, Lc, Li, lda, sA, sP, c, p, f, sZ, sR);
       else
-        update_eager<false>(Acc, Aic, Lc, Li, lda, sA, sP, c, p);
+        update_eager<false, NR>(Acc, Aic, Lc, Li, lda, sA, sP, c, p, f, sZ, sR);
     } else
 #endif
     {
+      // (the host folds the forward substitution only into schedules whose panels apply one column: kk == NB)
       Tile64 tl;
       update_to_lds(tl, Acc, lda, Lc, Lc, lda, kk, smem, sA);
       if (panel) {
@@ -218,6 +377,10 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
   } else {
     load_tile_lds(Acc, lda, sA);
     if (panel) load_tile_lds(Aic, lda, sP);
+    if constexpr (NR > 0) {
+      if (!panel)
+        for (int e = t; e < NB * NR; e += WG) sR[e] = fwd_y(f, e / NR, e % NR);  // r_0 = (Y - mean)_0
+    }
   }
   __syncthreads();
   GPX_PANEL_STAMP(0);
@@ -279,6 +442,11 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
           ++e;
         }
       }
+      if constexpr (NR > 0) {
+#ifndef GPX_FOLD_NO_P0
+        if (!panel) fwd_pivot_step<NR>(s, w, D, sA, sR, sZs, sZall);
+#endif
+      }
     }
     GPX_PANEL_STAMP(3 + 3 * s);
   }
@@ -291,12 +459,19 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
       const int r = e >> 6, cc = e & 63;
       Lcc[e] = (cc <= r) ? sA[r * LD64 + cc] : 0.0;
     }
+    if constexpr (NR > 0) {
+      for (int e = t; e < NB * NR; e += WG) f.z[(int64_t)c * NB * NR + e] = sZall[e];
+    }
     return;
   }
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int e = (t + q * WG) * 2, r = e >> 6, cc = e & 63;
     *reinterpret_cast<double2*>(Aic + (int64_t)r * lda + cc) = make_double2(sP[r * LD64 + cc], sP[r * LD64 + cc + 1]);
+  }
+  if constexpr (NR > 0) {
+    if (c > 0)
+      for (int e = t; e < NB * NR; e += WG) f.r[(int64_t)bi * NB * NR + e] = sR[e];
   }
 }
 
@@ -360,14 +535,24 @@ __device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t ld
     for (int j = 0; j < Tile128::WN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) cv[j][r] = C[(int64_t)Tile128::row_of(i, r) * lda + Tile128::col_of(j)];
+    // write-through 16-byte stores: adjacent lanes swap halves so that each lane holds two adjacent columns of one row
+    const rsrc_t rc = buf_rsrc(C);
+    const bool even = (threadIdx.x & 1) == 0;
 #pragma unroll
-    for (int j = 0; j < Tile128::WN; ++j)
+    for (int j = 0; j < Tile128::WN; ++j) {
+      double v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = Tile128::row_of(i, r), col = Tile128::col_of(j);
-        const int rb = r0 + (row >> 6), cb = q0 + (col >> 6);
-        if (cb >= cfirst && rb >= cb) C[(int64_t)row * lda + col] = cv[j][r] - tl.acc[i][j][r];
-      }
+      for (int r = 0; r < 4; ++r) v[r] = cv[j][r] - tl.acc[i][j][r];
+      const double x0 = swap_adjacent_lanes(even ? v[2] : v[0]);
+      const double x1 = swap_adjacent_lanes(even ? v[3] : v[1]);
+      const int col = Tile128::col_of(j) & ~1;
+      const int cb = q0 + (col >> 6);
+      const int ra = Tile128::row_of(i, even ? 0 : 2), rb2 = Tile128::row_of(i, even ? 1 : 3);
+      if (cb >= cfirst && r0 + (ra >> 6) >= cb)
+        st2_sc1(rc, (int)(((int64_t)ra * lda + col) * 8), even ? v[0] : x0, even ? x0 : v[2]);
+      if (cb >= cfirst && r0 + (rb2 >> 6) >= cb)
+        st2_sc1(rc, (int)(((int64_t)rb2 * lda + col) * 8), even ? v[1] : x1, even ? x1 : v[3]);
+    }
   }
 }
 
@@ -424,9 +609,12 @@ inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush,
   return s;
 }
 
+// NR: 0 = no forward fold, else its right-hand-side row length (one instantiation each: the fold's registers stay out
+// of the plain kernel)
+template <int NR>
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
 potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, StepPlan s, double* __restrict__ Dinv,
-                  int32_t* __restrict__ info, int first_wg, int64_t sa, int64_t sd) {
+                  int32_t* __restrict__ info, int first_wg, int64_t sa, int64_t sd, PotrfFwd f) {
   A += blockIdx.y * sa;  // problem of a batched fit
   Dinv += blockIdx.y * sd;
   info += blockIdx.y;
@@ -436,9 +624,14 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, StepPlan
   if (b >= s.npanel + s.nlook && b < s.tbase) return;  // alignment padding of the trailing workgroups
   const int role = b < s.npanel ? 0 : (b < s.npanel + s.nlook ? 1 : 2);
   GPX_STEP_STAMP(role, c, b, 0);
-  if (role == 0)
-    panel_role(A, lda, c, b, nblk, s.c0, Dinv, info, lds);
-  else if (role == 1)
+  if (role == 0) {
+    if constexpr (NR > 0) {
+      f.Y += blockIdx.y * f.sy;
+      f.r += blockIdx.y * f.sb;
+      f.z += blockIdx.y * f.sb;
+    }
+    panel_role<NR>(A, lda, c, b, nblk, s.c0, Dinv, info, lds, f);
+  } else if (role == 1)
     lookahead_role(A, lda, c, s.look_a, b - s.npanel, lds);
   else
     trailing_role(A, lda, c, nblk, s.k0, s.cfirst, b - s.tbase, s.ntrail, s.xmap, lds);
@@ -516,12 +709,17 @@ static void for_each_step(const Context* ctx, int nblk, int mode, int cend, F&& 
 }
 
 static void launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
-                         int cbeg, int cend) {
+                         int cbeg, int cend, const PotrfFwd& f = PotrfFwd()) {
   const int mode = potrf_mode(ctx, nblk);
   for_each_step(ctx, nblk, mode, cend, [&](int c, const StepPlan& s) {
     if (c < cbeg) return;
     const dim3 grid(s.tbase + s.ntrail, bt.count);
-    potrf_step_kernel<<<grid, WG, 0, ctx->stream>>>(A, lda, c, nblk, s, Dinv, info, 0, bt.k, bt.dinv);
+    if (!f.r)
+      potrf_step_kernel<0><<<grid, WG, 0, ctx->stream>>>(A, lda, c, nblk, s, Dinv, info, 0, bt.k, bt.dinv, f);
+    else if (f.nrhs == 1)
+      potrf_step_kernel<1><<<grid, WG, 0, ctx->stream>>>(A, lda, c, nblk, s, Dinv, info, 0, bt.k, bt.dinv, f);
+    else
+      potrf_step_kernel<GPX_MAX_RHS><<<grid, WG, 0, ctx->stream>>>(A, lda, c, nblk, s, Dinv, info, 0, bt.k, bt.dinv, f);
   });
 }
 
@@ -535,15 +733,35 @@ hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* 
                         double* W, int64_t ldw, const ForwardRhs* fr, bool* z_done) {
   LaunchTimer tm(ctx, GPX_TIMER_POTRF);
   const int nblk = npad / NB;
+  // the trailing tiles' write-through stores address a 128-row tile through a buffer descriptor (32-bit byte offsets)
+  if (lda > (int64_t(1) << 20)) return hipErrorInvalidValue;
   if (z_done) *z_done = false;
-  if (ctx->potrf_schedule != 1 && potrf_dag_workers(ctx, npad, bt.count) > 0) {
+  if (ctx->potrf_schedule == 2 && potrf_dag_workers(ctx, npad, bt.count) > 0) {
     hipError_t e = launch_potrf_dag(ctx, npad, A, lda, Dinv, info, bt, W, ldw, fr);
     if (e == hipSuccess && z_done && fr && fr->Y) *z_done = true;
     return e;
   }
-  launch_steps(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk);
+  PotrfFwd f;
+#if !defined(GPX_POTRF_TILE_PREUPDATE) && !defined(GPX_NO_FOLD)
+  // the fold needs panels that apply exactly one pending column per launch (eager or lookahead schedules)
+  if (fr && fr->Y && fr->buf && (potrf_mode(ctx, nblk) == 1 || potrf_lazy(ctx, nblk) == 1)) {
+    const int64_t nr = rhs_row(fr->nrhs);
+    f.Y = fr->Y;
+    f.ldy = fr->ldy;
+    f.sy = fr->sy;
+    f.r = fr->buf;
+    f.z = fr->buf + (int64_t)npad * nr;
+    f.sb = 2 * (int64_t)npad * nr;
+    f.nrhs = fr->nrhs;
+    f.n = fr->n;
+    f.mean = fr->mean;
+  }
+#endif
+  launch_steps(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, f);
   launch_dinv(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, W, ldw);
-  return hipGetLastError();
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess && z_done && f.r) *z_done = true;
+  return e;
 }
 
 }  // namespace gpx
