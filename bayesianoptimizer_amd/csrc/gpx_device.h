@@ -220,6 +220,31 @@ struct MfmaTile {
     }
   }
 
+  // The same accumulation with the last k-tile peeled: before_last() runs right before its MFMAs, when no staging loads
+  // are in flight and the staging registers are dead, so an epilogue's first global loads overlap that k-tile without
+  // holding registers across the loop (kend > kbeg).
+  template <typename F>
+  __device__ __forceinline__ void run_acc_peeled(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
+                                                 int64_t ldb, int kbeg, int kend, double* smem, F&& before_last) {
+    double* cur = smem;
+    double* nxt = smem + BK * (PA + PB);
+    load_regs(A, lda, B, ldb, kbeg);
+    store_lds(cur, cur + BK * PA);
+    __syncthreads();
+    for (int k0 = kbeg; k0 + BK < kend; k0 += BK) {
+      load_regs(A, lda, B, ldb, k0 + BK);
+      compute(cur, cur + BK * PA);
+      store_lds(nxt, nxt + BK * PA);
+      __syncthreads();
+      double* t = cur;
+      cur = nxt;
+      nxt = t;
+    }
+    before_last();
+    compute(cur, cur + BK * PA);
+    __syncthreads();
+  }
+
   // Row / column of accumulator element (i, j, r) for this lane, relative to the tile origin.
   __device__ __forceinline__ static int row_of(int i, int r) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

@@ -106,6 +106,24 @@ __device__ __forceinline__ double swap_adjacent_lanes(double v) {  // DPP quad_p
   return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
+// One 16x16 accumulator block (i, j) of an MfmaTile (rows row_of(i, r), column col_of(j)) stored write-through as 16-byte
+// pairs: adjacent lanes swap halves so that the even lane holds two adjacent columns of rows r = 0, 1 and the odd lane of
+// rows r = 2, 3 (sc1 stores leave no dirty line in the XCD's L2 for the kernel boundary to write back).  keep01 / keep23:
+// store the even / odd lane's rows.
+template <typename T>
+__device__ __forceinline__ void store_block_pairs_sc1(rsrc_t rc, int64_t ld, int i, int j, const d4& v, bool keep01,
+                                                      bool keep23) {
+  const bool even = (threadIdx.x & 1) == 0;
+  const double x0 = swap_adjacent_lanes(even ? v[2] : v[0]);
+  const double x1 = swap_adjacent_lanes(even ? v[3] : v[1]);
+  const int col = T::col_of(j) & ~1;
+  const int ra = T::row_of(i, even ? 0 : 2), rb = T::row_of(i, even ? 1 : 3);
+  if (even ? keep01 : keep23) {
+    st2_sc1(rc, (int)(((int64_t)ra * ld + col) * 8), even ? v[0] : x0, even ? x0 : v[2]);
+    st2_sc1(rc, (int)(((int64_t)rb * ld + col) * 8), even ? v[1] : x1, even ? x1 : v[3]);
+  }
+}
+
 // The forward half of alpha's triangular solve folded into the factorisation (launch_potrf with a ForwardRhs, eager
 // schedules only): z = L^{-1} (Y - mean) for NR = 1 or GPX_MAX_RHS right-hand-side columns (padded rows and columns
 // >= nrhs are 0).  Row block i's running right-hand side r_i = (Y - mean)_i - sum_{k < c} L_ik z_k is kept by the panel
@@ -464,10 +482,11 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
     }
     return;
   }
+  const rsrc_t ra = buf_rsrc(Aic);
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int e = (t + q * WG) * 2, r = e >> 6, cc = e & 63;
-    *reinterpret_cast<double2*>(Aic + (int64_t)r * lda + cc) = make_double2(sP[r * LD64 + cc], sP[r * LD64 + cc + 1]);
+    st2_sc1(ra, (int)(((int64_t)r * lda + cc) * 8), sP[r * LD64 + cc], sP[r * LD64 + cc + 1]);
   }
   if constexpr (NR > 0) {
     if (c > 0)
@@ -525,33 +544,36 @@ __device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t ld
   const double* Lj = A + (int64_t)q0 * NB * lda + (int64_t)k0 * NB;
   double* C = A + (int64_t)r0 * NB * lda + (int64_t)q0 * NB;
   Tile128 tl;
-  tl.run(Li, lda, Lj, lda, 0, (c - k0) * NB, lds);
-  // C - acc, stored for the 64-blocks (rb, cb) with cb >= c+1 and rb >= cb; loads of a row group first (seeding acc with
-  // -C before the product, as the 64x64 panel updates do, pushes this 128x128 tile into 30 VGPR spills)
-#pragma unroll
-  for (int i = 0; i < Tile128::WM; ++i) {
-    double cv[Tile128::WN][4];
+  // C - acc, stored for the 64-blocks (rb, cb) with cb >= c+1 and rb >= cb, one row group i at a time: row group 0's C
+  // loads are issued before the last k-tile's MFMAs and group i+1's before group i's stores, so one load round trip is
+  // exposed instead of one per group (seeding acc with -C before the product, as the 64x64 panel updates do, pushes this
+  // 128x128 tile into 30 VGPR spills)
+  double cv[Tile128::WN][4];
+  auto load_group = [&](int i) {
 #pragma unroll
     for (int j = 0; j < Tile128::WN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) cv[j][r] = C[(int64_t)Tile128::row_of(i, r) * lda + Tile128::col_of(j)];
-    // write-through 16-byte stores: adjacent lanes swap halves so that each lane holds two adjacent columns of one row
-    const rsrc_t rc = buf_rsrc(C);
-    const bool even = (threadIdx.x & 1) == 0;
+  };
+  tl.zero();
+  tl.run_acc_peeled(Li, lda, Lj, lda, 0, (c - k0) * NB, lds, [&] { load_group(0); });
+  const rsrc_t rc = buf_rsrc(C);
+#pragma unroll
+  for (int i = 0; i < Tile128::WM; ++i) {
+#pragma unroll
+    for (int j = 0; j < Tile128::WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tl.acc[i][j][r] = cv[j][r] - tl.acc[i][j][r];
+    if (i + 1 < Tile128::WM) load_group(i + 1);
+    // write-through 16-byte pairs; a 16-column pair never straddles a 64-block, and rows r = 0, 1 (even lanes) or 2, 3
+    // (odd lanes) of one lane lie in one 64-row block
 #pragma unroll
     for (int j = 0; j < Tile128::WN; ++j) {
-      double v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = cv[j][r] - tl.acc[i][j][r];
-      const double x0 = swap_adjacent_lanes(even ? v[2] : v[0]);
-      const double x1 = swap_adjacent_lanes(even ? v[3] : v[1]);
-      const int col = Tile128::col_of(j) & ~1;
-      const int cb = q0 + (col >> 6);
-      const int ra = Tile128::row_of(i, even ? 0 : 2), rb2 = Tile128::row_of(i, even ? 1 : 3);
-      if (cb >= cfirst && r0 + (ra >> 6) >= cb)
-        st2_sc1(rc, (int)(((int64_t)ra * lda + col) * 8), even ? v[0] : x0, even ? x0 : v[2]);
-      if (cb >= cfirst && r0 + (rb2 >> 6) >= cb)
-        st2_sc1(rc, (int)(((int64_t)rb2 * lda + col) * 8), even ? v[1] : x1, even ? x1 : v[3]);
+      const int cb = q0 + (Tile128::col_of(j) >> 6);
+      const bool colok = cb >= cfirst;
+      const bool k01 = colok && r0 + (Tile128::row_of(i, 0) >> 6) >= cb;
+      const bool k23 = colok && r0 + (Tile128::row_of(i, 2) >> 6) >= cb;
+      store_block_pairs_sc1<Tile128>(rc, lda, i, j, tl.acc[i][j], k01, k23);
     }
   }
 }
@@ -568,12 +590,14 @@ __device__ __forceinline__ void lookahead_role(double* __restrict__ A, int64_t l
   Tile64 tl;
   tl.load_neg_c(C, lda);
   tl.run_acc(Li, lda, Lj, lda, 0, (c - a) * NB, lds);
+  const rsrc_t rc = buf_rsrc(C);
 #pragma unroll
   for (int ii = 0; ii < Tile64::WM; ++ii)
 #pragma unroll
-    for (int jj = 0; jj < Tile64::WN; ++jj)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) C[(int64_t)Tile64::row_of(ii, r) * lda + Tile64::col_of(jj)] = -tl.acc[ii][jj][r];
+    for (int jj = 0; jj < Tile64::WN; ++jj) {
+      const d4 v = -tl.acc[ii][jj];
+      store_block_pairs_sc1<Tile64>(rc, lda, ii, jj, v, true, true);
+    }
 }
 
 // Work split of launch c.  Flush launches (plan.flush) apply the columns k0 .. c-1 (k0 = the previous flush launch, or 0)
