@@ -1,5 +1,5 @@
-"""The persistent dataflow Cholesky (gpx_potrf_dag.hip, the default for padded n <= 4096) against the multi-launch
-schedule and the oracle; failure reporting of the two persistent launches (dataflow Cholesky, triangular solve) when an
+"""The persistent dataflow Cholesky (gpx_potrf_dag.hip, opt-in: potrf_schedule = 2; measured slower than the default
+multi-launch schedule) against the multi-launch schedule and the oracle; failure reporting of the two persistent launches (dataflow Cholesky, triangular solve) when an
 in-launch hand-off times out; the per-handle options that replaced the library's environment knobs (include/gpx.h
 GPX_OPT_*).  Reference call sites: psd_safe_cholesky [upstream] reached from optimization/Bayesian.py:89-94, jitter
 retry optimization/Bayesian6.py:481-488."""
@@ -69,18 +69,22 @@ def test_dataflow_not_pd_pivot_deep(engine):
 
 
 def test_fit_timeout_raises_timeout_error_not_not_pd(engine):
-    """spin_limit = 0: every in-launch wait gives up at its first unmet poll.  The dataflow Cholesky's pool tasks wait
-    for the chain from the start, so the factorisation reports GPX_INFO_TIMEOUT; the fit raises GPXTimeoutError (a
-    jitter retry would not cure it), and the next call with the default limit is correct again."""
+    """spin_limit = 0: every in-launch wait gives up at its first unmet poll.  Under both schedules the fit raises
+    GPXTimeoutError (dataflow: the pool tasks wait for the chain from the start; multi-launch: the backward solve's
+    hand-offs), never NotPositiveDefiniteError (a jitter retry would not cure it), and the next call with the default
+    limit is correct again."""
     n = 4096
     X, y = O.synthetic_problem(n, 8, 21)
     kp, _ = pair("rbf", 8, noise=1e-4)
-    engine.set_option("spin_limit", 0)
-    try:
-        with pytest.raises(GPXTimeoutError):
-            engine.fit(t(X), t(y), kp)
-    finally:
-        engine.set_option("spin_limit", 1 << 22)
+    for schedule in (0, 2):
+        engine.set_option("potrf_schedule", schedule)
+        engine.set_option("spin_limit", 0)
+        try:
+            with pytest.raises(GPXTimeoutError):
+                engine.fit(t(X), t(y), kp)
+        finally:
+            engine.set_option("spin_limit", 1 << 22)
+            engine.set_option("potrf_schedule", 0)
     st = engine.fit(t(X), t(y), kp)
     assert st.pivot_failure() == -1
 
@@ -150,12 +154,17 @@ def test_options_from_environment_at_create():
 
 def test_fit_results_identical_across_pool_sizes(engine):
     """The dataflow schedule decides who runs a task, never how: a batched fit (64 workgroups per problem) equals the
-    single fit (256 workgroups) bit for bit at n = 4096."""
+    single fit (256 workgroups) bit for bit at n = 4096; so does the default multi-launch schedule."""
     n = 4096
     X, y = O.synthetic_problem(n, 8, 40)
     kp, _ = pair("rbf", 8, noise=1e-4)
-    st = engine.fit(t(X), t(y), kp)
-    L1 = st.L.cpu().numpy().copy()
-    sts = engine.fit_batched(t(np.stack([X] * 4)), t(np.stack([y] * 4)), kp)
-    for s in sts:
-        np.testing.assert_array_equal(np.tril(s.L.cpu().numpy()), np.tril(L1))
+    for schedule in (2, 0):
+        engine.set_option("potrf_schedule", schedule)
+        try:
+            st = engine.fit(t(X), t(y), kp)
+            L1 = st.L.cpu().numpy().copy()
+            sts = engine.fit_batched(t(np.stack([X] * 4)), t(np.stack([y] * 4)), kp)
+            for s in sts:
+                np.testing.assert_array_equal(np.tril(s.L.cpu().numpy()), np.tril(L1))
+        finally:
+            engine.set_option("potrf_schedule", 0)
