@@ -76,16 +76,23 @@ def barrier(dist):
     torch.cuda.synchronize()
 
 
-def pmc_traffic_per_launch():
-    """HBM bytes per trmm launch from the committed rocprofv3 --pmc passes (tools/pmc_traffic.py)."""
-    path = os.path.join(ROOT, "profiles", "trmm_pmc_traffic.json")
+PMC_TRAFFIC_FILE = os.path.join("profiles", "trmm_pmc_traffic.json")
+
+
+def pmc_traffic_record():
+    """HBM bytes per trmm launch from the rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.py; the
+    round check runs them right before this bench on the same box and tree), and where that number came from."""
+    path = os.path.join(ROOT, PMC_TRAFFIC_FILE)
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            rec = json.load(f)
     except Exception:
-        return None
+        return None, None
+    src = {"file": PMC_TRAFFIC_FILE, "generated_utc": rec.get("generated_utc"), "dispatches": rec.get("dispatches"),
+           "passes": rec.get("passes")}
+    return rec.get("hbm_bytes_per_launch"), src
 
 
 def _torch_cpu_step(X, y, Xs, ls, noise, best_f, kind):
@@ -505,6 +512,7 @@ def main():
         extra = None
         if world == 1 and not args.no_other_configs:
             extra = other_configs(eng, dev, args.seed)
+        traffic, traffic_src = pmc_traffic_record()
         out = {
             "metric": METRIC,
             "value": value,
@@ -546,7 +554,8 @@ def main():
                 "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / FP64_PEAK_TFLOPS,
-                "traffic": pmc_traffic_per_launch(),
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "avg_launch_ms": avg_ms,
                 "launches": trmm_launches,
                 "flops_per_launch": flops_per_launch,
