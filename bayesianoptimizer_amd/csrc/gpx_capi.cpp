@@ -58,6 +58,9 @@ gpx_status check_n(Context* c, int64_t n) {
 gpx_status check_ld(Context* c, int64_t ld, int64_t minimum, const char* name, bool even) {
   if (ld < minimum) return fail(c, GPX_INVALID_ARG, std::string(name) + " leading dimension too small");
   if (even && (ld & 1)) return fail(c, GPX_INVALID_ARG, std::string(name) + " leading dimension must be even");
+  // the matrix kernels address 128-row tiles through buffer descriptors with 32-bit byte offsets
+  if (even && ld > GPX_MAX_LD)
+    return fail(c, GPX_INVALID_ARG, std::string(name) + " leading dimension above GPX_MAX_LD (2^20)");
   return GPX_OK;
 }
 

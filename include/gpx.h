@@ -35,6 +35,7 @@ extern "C" {
 #define GPX_MAX_DIM 32
 #define GPX_MAX_RHS 8
 #define GPX_TILE 128
+#define GPX_MAX_LD (1 << 20)            /* leading dimension limit of the matrix arguments (K, L, W) */
 #define GPX_MAX_Q 32                    /* q-batch size of gpx_moments_grad_f64 */
 #define GPX_MAX_GRAD_CANDIDATES 16384  /* candidates per gpx_moments_grad_f64 call */
 

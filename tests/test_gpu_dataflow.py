@@ -168,3 +168,18 @@ def test_fit_results_identical_across_pool_sizes(engine):
                 np.testing.assert_array_equal(np.tril(s.L.cpu().numpy()), np.tril(L1))
         finally:
             engine.set_option("potrf_schedule", 0)
+
+
+def test_matrix_leading_dimension_limit(engine):
+    """Matrix leading dimensions above GPX_MAX_LD (2^20: the tile stores use buffer descriptors with 32-bit byte
+    offsets) are rejected with GPX_INVALID_ARG before anything runs; the pointers are never dereferenced."""
+    K = torch.zeros(128, 128, dtype=torch.float64, device=engine.device)
+    Dinv = torch.zeros(4, 64, 64, dtype=torch.float64, device=engine.device)  # 2 (npad / 64) blocks
+    info = torch.zeros(1, dtype=torch.int32, device=engine.device)
+    p = lambda x: x.data_ptr()
+    st = engine.lib.gpx_potrf_f64(engine.handle, 128, p(K), (1 << 20) + 2, p(Dinv), p(info))
+    assert st == _capi.GPX_INVALID_ARG
+    assert b"GPX_MAX_LD" in engine.lib.gpx_last_error(engine.handle)
+    assert engine.lib.gpx_potrf_f64(engine.handle, 128, p(K), 128, p(Dinv), p(info)) == _capi.GPX_OK
+    torch.cuda.synchronize()
+    assert int(info.item()) != 0  # the all-zero matrix is not positive definite
