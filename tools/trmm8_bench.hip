@@ -163,9 +163,11 @@ int main() {
     if (which == 1) trmm_w<2, 4, 4><<<grid, 512>>>(W, n, K, C, nI, ss1);  // 8 waves of 64 x 32
     if (which == 2) trmm_w<4, 2, 4><<<grid, 512>>>(W, n, K, C, nI, ss1);  // 8 waves of 32 x 64
     if (which == 3) trmm_w<2, 2, 2><<<grid, 256>>>(W, n, K, C, nI, ss1);  // shipped shape again
+    if (which == 4) trmm_w<4, 4, 8><<<grid, 1024>>>(W, n, K, C, nI, ss1);  // 16 waves of 32 x 32
   };
-  const char* names[] = {"4 waves 64x64 (shipped shape)", "8 waves 64x32", "8 waves 32x64", "4 waves again"};
-  const int NV = 4;
+  const char* names[] = {"4 waves 64x64 (old shape)", "8 waves 64x32", "8 waves 32x64", "4 waves again",
+                         "16 waves 32x32"};
+  const int NV = 5;
   const double flops = (double)n * n * C;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
