@@ -190,31 +190,39 @@ __device__ __forceinline__ void wave_matvec16(const double* M, int ldm, const do
 // the compiler from moving the reads up)
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-template <int W, bool PANEL, int NR>
+// HALF (p > 0 only): the workgroup owns 32 rows of A_ic (row blocks RB = 0, 1 of the half); wave W then updates A_ic
+// blocks (W >> 1, 2 (W & 1) + jj), jj = 0, 1, beside its A_cc blocks: at most 5 blocks per wave instead of 7.
+template <int W, bool PANEL, int NR, bool HALF>
 __device__ __forceinline__ void update_eager_wave(const double* __restrict__ Acc, const double* __restrict__ Aic,
                                                   const double* __restrict__ Lc, const double* __restrict__ Li,
-                                                  int64_t lda, double* sA, double* sP, int c, int p,
+                                                  int64_t lda, double* sA, double* sP, int c, int rowblk0,
                                                   const PotrfFwd& f, double* sZ, double* sR) {
   constexpr int NCC = W < 2 ? 3 : 2;
+  constexpr int NIC = HALF ? 2 : 4;             // A_ic blocks of this wave
+  constexpr int RB = HALF ? (W >> 1) : W;       // its A_ic row block (within the workgroup's rows)
+  constexpr int JB0 = HALF ? 2 * (W & 1) : 0;   // its first A_ic column block
+  constexpr int NRI = HALF ? 4 : 8;             // double2 loads of L_i per thread (32 or 64 rows)
+  constexpr bool FOLD_ROWS = !PANEL || !HALF || (W & 1) == 0;  // waves that fold their row block's right-hand side
   const int t = threadIdx.x, lane = t & 63;
   const int g = lane >> 4, cl = lane & 15;
-  double2 rl[8], ri[8];
-  d4 acc_cc[NCC], acc_ic[4];
-  // forward fold: z_{c-1} (-> LDS sZ) and this lane's old right-hand sides (row 16 W + cl of block c + p)
+  double2 rl[8], ri[NRI];
+  d4 acc_cc[NCC], acc_ic[NIC];
+  // forward fold: z_{c-1} (-> LDS sZ) and this lane's old right-hand sides (row 16 RB + cl of the workgroup's rows,
+  // which start at global row rowblk0)
   double2 zv = make_double2(0.0, 0.0);
   double rold[NR > 0 ? NR : 1];
-  const int frow = (c + p) * NB + 16 * W + cl;
+  const int frow = rowblk0 + 16 * RB + cl;
   if constexpr (NR > 0) {
     if (t < 32 * NR) zv = *reinterpret_cast<const double2*>(f.z + (int64_t)(c - 1) * NB * NR + 2 * t);
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr)
-      rold[rr] = g != 0 ? 0.0 : (c == 1 ? fwd_y(f, frow, rr) : f.r[(int64_t)frow * NR + rr]);
+      rold[rr] = (g != 0 || !FOLD_ROWS) ? 0.0 : (c == 1 ? fwd_y(f, frow, rr) : f.r[(int64_t)frow * NR + rr]);
   }
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int e = (t + q * WG) * 2, r = e >> 6, cc = e & 63;
     rl[q] = *reinterpret_cast<const double2*>(Lc + (int64_t)r * lda + cc);
-    if (PANEL) ri[q] = *reinterpret_cast<const double2*>(Li + (int64_t)r * lda + cc);
+    if (PANEL && q < NRI) ri[q] = *reinterpret_cast<const double2*>(Li + (int64_t)r * lda + cc);
   }
 #pragma unroll
   for (int b = 0; b < NCC; ++b) {
@@ -224,21 +232,21 @@ __device__ __forceinline__ void update_eager_wave(const double* __restrict__ Acc
   }
   if (PANEL) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NIC; ++j)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc_ic[j][q] = Aic[(int64_t)(16 * W + g + 4 * q) * lda + 16 * j + cl];
+      for (int q = 0; q < 4; ++q) acc_ic[j][q] = Aic[(int64_t)(16 * RB + g + 4 * q) * lda + 16 * (JB0 + j) + cl];
   }
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int e = (t + q * WG) * 2, r = e >> 6, cc = e & 63;
     *reinterpret_cast<double2*>(sA + r * LD64 + cc) = rl[q];
-    if (PANEL) *reinterpret_cast<double2*>(sP + r * LD64 + cc) = ri[q];
+    if (PANEL && q < NRI) *reinterpret_cast<double2*>(sP + r * LD64 + cc) = ri[q];
   }
   if constexpr (NR > 0) {
     if (t < 32 * NR) *reinterpret_cast<double2*>(sZ + 2 * t) = zv;
   }
   __syncthreads();
-  GPX_EAGER_STAMP(c, p, 0);
+  GPX_EAGER_STAMP(c, rowblk0, 0);
   // k in chunks of 16: one batch of fragment reads (the four L_c row blocks serve as the B operand of every block and as
   // the A operand of the A_cc blocks; L_i's row block W is A_ic's A operand), then the chunk's MFMAs, independent
   // across blocks
@@ -255,54 +263,54 @@ __device__ __forceinline__ void update_eager_wave(const double* __restrict__ Acc
     for (int s = 0; s < 4; ++s) {
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) fc[jb][s] = sA[(16 * jb + m) * LD64 + kc + 4 * s + kq];
-      if (PANEL) fi[s] = sP[(16 * W + m) * LD64 + kc + 4 * s + kq];
+      if (PANEL) fi[s] = sP[(16 * RB + m) * LD64 + kc + 4 * s + kq];
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       if (PANEL) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc_ic[j] = mfma_sub(fi[s], fc[j][s], acc_ic[j]);
+        for (int j = 0; j < NIC; ++j) acc_ic[j] = mfma_sub(fi[s], fc[JB0 + j][s], acc_ic[j]);
       }
 #pragma unroll
       for (int b = 0; b < NCC; ++b)
         acc_cc[b] = mfma_sub(fc[kLowerBlk[W + 4 * b][0]][s], fc[kLowerBlk[W + 4 * b][1]][s], acc_cc[b]);
-      if constexpr (NR > 0) {
+      if constexpr (NR > 0 && FOLD_ROWS) {
         const double lv = PANEL ? fi[s] : fc[W][s];
 #pragma unroll
         for (int rr = 0; rr < NR; ++rr) part[rr] = fma(lv, sZ[(kc + 4 * s + kq) * NR + rr], part[rr]);
       }
     }
   }
-  if constexpr (NR > 0) {
+  if constexpr (NR > 0 && FOLD_ROWS) {
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr) part[rr] = rowsum4(part[rr]);
     if (g == 0) {
 #pragma unroll
       for (int rr = 0; rr < NR; ++rr) {
-        sR[(16 * W + cl) * NR + rr] = rold[rr] - part[rr];  // stored to global memory at the workgroup's end
+        sR[(16 * RB + cl) * NR + rr] = rold[rr] - part[rr];  // stored to global memory at the workgroup's end
       }
     }
   }
   __syncthreads();  // every wave's operand reads done: sA / sP take the results
-  GPX_EAGER_STAMP(c, p, 1);
+  GPX_EAGER_STAMP(c, rowblk0, 1);
 #pragma unroll
   for (int b = 0; b < NCC; ++b) store_block16(sA, 16 * kLowerBlk[W + 4 * b][0], 16 * kLowerBlk[W + 4 * b][1], acc_cc[b]);
   if (PANEL) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) store_block16(sP, 16 * W, 16 * j, acc_ic[j]);
+    for (int j = 0; j < NIC; ++j) store_block16(sP, 16 * RB, 16 * (JB0 + j), acc_ic[j]);
   }
 }
 
-template <bool PANEL, int NR>
+template <bool PANEL, int NR, bool HALF>
 __device__ __forceinline__ void update_eager(const double* __restrict__ Acc, const double* __restrict__ Aic,
                                              const double* __restrict__ Lc, const double* __restrict__ Li, int64_t lda,
-                                             double* sA, double* sP, int c, int p, const PotrfFwd& f, double* sZ,
+                                             double* sA, double* sP, int c, int rowblk0, const PotrfFwd& f, double* sZ,
                                              double* sR) {
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {  // wave-uniform: compile-time block lists per wave
-    case 0: update_eager_wave<0, PANEL, NR>(Acc, Aic, Lc, Li, lda, sA, sP, c, p, f, sZ, sR); break;
-    case 1: update_eager_wave<1, PANEL, NR>(Acc, Aic, Lc, Li, lda, sA, sP, c, p, f, sZ, sR); break;
-    case 2: update_eager_wave<2, PANEL, NR>(Acc, Aic, Lc, Li, lda, sA, sP, c, p, f, sZ, sR); break;
-    default: update_eager_wave<3, PANEL, NR>(Acc, Aic, Lc, Li, lda, sA, sP, c, p, f, sZ, sR); break;
+    case 0: update_eager_wave<0, PANEL, NR, HALF>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
+    case 1: update_eager_wave<1, PANEL, NR, HALF>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
+    case 2: update_eager_wave<2, PANEL, NR, HALF>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
+    default: update_eager_wave<3, PANEL, NR, HALF>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
   }
 }
 
@@ -334,10 +342,11 @@ __device__ __forceinline__ void fwd_pivot_step(int s, int w, const double* D, co
   }
 }
 
+template <int ROWS = NB>
 __device__ __forceinline__ void load_tile_lds(const double* __restrict__ G, int64_t ld, double* S) {
   const int t = threadIdx.x;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < ROWS / 8; ++q) {
     const int e = (t + q * WG) * 2, r = e >> 6, c = e & 63;
     const double2 v = *reinterpret_cast<const double2*>(G + (int64_t)r * ld + c);
     S[r * LD64 + c] = v.x;
@@ -345,11 +354,15 @@ __device__ __forceinline__ void load_tile_lds(const double* __restrict__ G, int6
   }
 }
 
-// Panel workgroup p of block column c (see the file comment); NR > 0: with the forward fold (PotrfFwd).
-template <int NR>
-__device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, int c, int p, int nblk, int c0,
+// Panel workgroup p of block column c (see the file comment); NR > 0: with the forward fold (PotrfFwd).  HALF (p > 0):
+// the workgroup owns rows 32 h .. 32 h + 31 of row block c + p (a 96-row tall panel), so that its pre-update and its T /
+// U items are two thirds of a full one; the host splits the row blocks this way where the launch still fits the
+// co-resident slots (StepPlan::half).
+template <int NR, bool HALF>
+__device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, int c, int p, int h, int nblk, int c0,
                                            double* __restrict__ Dinv, int32_t* __restrict__ info, double* lds,
                                            const PotrfFwd& f) {
+  constexpr int PROWS = HALF ? NB / 2 : NB;  // rows of A_ic this workgroup owns
   double* sA = lds;             // A_cc -> L_cc
   double* sP = sA + NB * LD64;  // A_ic -> L_ic (p > 0)
   double* sDb = sP + NB * LD64; // D_ss, double-buffered by step parity (2 x 16 x LDD)
@@ -364,26 +377,28 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
   double* sZall = sP + NB * GPX_MAX_RHS;
   double* sZs = sZall + NB * GPX_MAX_RHS;  // one 16 x NR slot per wave 1..3
   static_assert(NB * GPX_MAX_RHS <= DBUF && 2 * NB * GPX_MAX_RHS + 3 * 16 * GPX_MAX_RHS <= NB * LD64, "fold LDS");
-  const int nrow = panel ? 8 : 4;  // 16-row blocks of the tall panel
+  const int nrow = panel ? 4 + PROWS / 16 : 4;  // 16-row blocks of the tall panel
   const int bi = c + p;
+  const int row0 = bi * NB + (HALF ? PROWS * h : 0);  // first global row of this workgroup's A_ic rows
   const double* Acc = A + (int64_t)c * NB * lda + (int64_t)c * NB;
-  double* Aic = A + (int64_t)bi * NB * lda + (int64_t)c * NB;
+  double* Aic = A + (int64_t)row0 * lda + (int64_t)c * NB;
   if (t == 0) s_tdone = 0;
   if (c > 0) {
     // the updates of block columns c0 .. c-1 not yet applied to this column, on the two tiles this workgroup
     // factors (K = 64 (c - c0))
     const int kk = (c - c0) * NB;
     const double* Lc = A + (int64_t)c * NB * lda + (int64_t)c0 * NB;
-    const double* Li = A + (int64_t)bi * NB * lda + (int64_t)c0 * NB;
+    const double* Li = A + (int64_t)row0 * lda + (int64_t)c0 * NB;
 #ifndef GPX_POTRF_TILE_PREUPDATE
     if (kk == NB) {
       if (panel)
-        update_eager<true, NR>(Acc, Aic, Lc, Li, lda, sA, sP, c, p, f, sZ, sR);
+        update_eager<true, NR, HALF>(Acc, Aic, Lc, Li, lda, sA, sP, c, row0, f, sZ, sR);
       else
-        update_eager<false, NR>(Acc, Aic, Lc, Li, lda, sA, sP, c, p, f, sZ, sR);
+        update_eager<false, NR, false>(Acc, Aic, Lc, Li, lda, sA, sP, c, c * NB, f, sZ, sR);
     } else
 #endif
     {
+      // (never HALF: the host splits panels only in schedules whose panels apply one column)
       // (the host folds the forward substitution only into schedules whose panels apply one column: kk == NB)
       Tile64 tl;
       update_to_lds(tl, Acc, lda, Lc, Lc, lda, kk, smem, sA);
@@ -394,7 +409,7 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
     }
   } else {
     load_tile_lds(Acc, lda, sA);
-    if (panel) load_tile_lds(Aic, lda, sP);
+    if (panel) load_tile_lds<PROWS>(Aic, lda, sP);
     if constexpr (NR > 0) {
       if (!panel)
         for (int e = t; e < NB * NR; e += WG) sR[e] = fwd_y(f, e / NR, e % NR);  // r_0 = (Y - mean)_0
@@ -484,13 +499,13 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
   }
   const rsrc_t ra = buf_rsrc(Aic);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < PROWS / 8; ++q) {
     const int e = (t + q * WG) * 2, r = e >> 6, cc = e & 63;
     st2_sc1(ra, (int)(((int64_t)r * lda + cc) * 8), sP[r * LD64 + cc], sP[r * LD64 + cc + 1]);
   }
   if constexpr (NR > 0) {
     if (c > 0)
-      for (int e = t; e < NB * NR; e += WG) f.r[(int64_t)bi * NB * NR + e] = sR[e];
+      for (int e = t; e < PROWS * NR; e += WG) f.r[(int64_t)row0 * NR + e] = sR[e];
   }
 }
 
@@ -607,11 +622,15 @@ __device__ __forceinline__ void lookahead_role(double* __restrict__ A, int64_t l
 struct StepPlan {
   int npanel, nlook, ntrail, c0, look_a, cfirst, k0, flush;
   int tbase, xmap;  // first trailing workgroup (a multiple of 8 when xmap: XCD-chunked tile order), tile order
+  int half;         // panel row blocks c+1.. split into two 32-row workgroups (panel workgroup b > 0: p = 1 + (b-1)/2)
 };
 
-inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush, int xmap = 0) {
+// slots > 0: the co-resident workgroup slots a problem may fill (two per CU, shared by a batch); the panel row blocks are
+// split in halves (StepPlan::half) when the panels apply exactly one column and the split launch still fits them.
+inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush, int xmap = 0, int slots = 0) {
   StepPlan s;
   s.npanel = nblk - c;
+  s.half = 0;
   s.flush = flush ? 1 : 0;
   s.k0 = last_flush;
   if (mode == 0) {
@@ -629,6 +648,15 @@ inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush,
   const int M = (flush && m > 0) ? (m + 1) / 2 : 0;
   s.ntrail = M * (M + 1) / 2;
   s.xmap = xmap;
+  const bool eager = mode == 1 || c == 0 || c - last_flush == 1;
+  if (slots > 0 && eager && s.npanel > 1) {
+    const int np = 1 + 2 * (s.npanel - 1);
+    const int tb = xmap ? (np + s.nlook + 7) & ~7 : np + s.nlook;
+    if (tb + s.ntrail <= slots) {
+      s.half = 1;
+      s.npanel = np;
+    }
+  }
   s.tbase = xmap ? (s.npanel + s.nlook + 7) & ~7 : s.npanel + s.nlook;  // padding workgroups exit at once
   return s;
 }
@@ -654,7 +682,10 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, StepPlan
       f.r += blockIdx.y * f.sb;
       f.z += blockIdx.y * f.sb;
     }
-    panel_role<NR>(A, lda, c, b, nblk, s.c0, Dinv, info, lds, f);
+    if (s.half && b > 0)
+      panel_role<NR, true>(A, lda, c, 1 + ((b - 1) >> 1), (b - 1) & 1, nblk, s.c0, Dinv, info, lds, f);
+    else
+      panel_role<NR, false>(A, lda, c, b, 0, nblk, s.c0, Dinv, info, lds, f);
   } else if (role == 1)
     lookahead_role(A, lda, c, s.look_a, b - s.npanel, lds);
   else
@@ -722,20 +753,35 @@ static int potrf_mode(const Context* ctx, int nblk) {
 
 // The plan of every launch c < cend (flush launches: c >= 1 and at least one interval after the previous flush).
 template <typename F>
-static void for_each_step(const Context* ctx, int nblk, int mode, int cend, F&& f) {
+static void for_each_step(const Context* ctx, int nblk, int mode, int cend, int slots, F&& f) {
   const int g = potrf_lazy(ctx, nblk);
   int last = 0;
   for (int c = 0; c < cend; ++c) {
     const bool flush = c >= 1 && c - last >= g;
-    f(c, step_plan(c, nblk, mode, last, flush, 1));
+    f(c, step_plan(c, nblk, mode, last, flush, 1, slots));
     if (flush) last = c;
   }
+}
+
+// Co-resident workgroup slots per problem (two per CU at the step kernel's LDS size, shared by the batch), or 0 when
+// the device cannot be queried (no half-panel split then).
+static int potrf_slots(Context* ctx, int batch) {
+#ifdef GPX_NO_HALF
+  return 0;
+#endif
+  if (ctx->cu_count <= 0) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    ctx->cu_count = cus;
+  }
+  return 2 * ctx->cu_count / (batch > 0 ? batch : 1);
 }
 
 static void launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
                          int cbeg, int cend, const PotrfFwd& f = PotrfFwd()) {
   const int mode = potrf_mode(ctx, nblk);
-  for_each_step(ctx, nblk, mode, cend, [&](int c, const StepPlan& s) {
+  for_each_step(ctx, nblk, mode, cend, potrf_slots(ctx, bt.count), [&](int c, const StepPlan& s) {
     if (c < cbeg) return;
     const dim3 grid(s.tbase + s.ntrail, bt.count);
     if (!f.r)
