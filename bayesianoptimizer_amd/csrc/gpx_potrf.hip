@@ -190,19 +190,20 @@ __device__ __forceinline__ void wave_matvec16(const double* M, int ldm, const do
 // the compiler from moving the reads up)
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// HALF (p > 0 only): the workgroup owns 32 rows of A_ic (row blocks RB = 0, 1 of the half); wave W then updates A_ic
-// blocks (W >> 1, 2 (W & 1) + jj), jj = 0, 1, beside its A_cc blocks: at most 5 blocks per wave instead of 7.
-template <int W, bool PANEL, int NR, bool HALF>
+// SPLIT (p > 0 only; 1, 2 or 4): the workgroup owns 64 / SPLIT rows of A_ic (its row blocks RB = 0 .. 4 / SPLIT - 1);
+// SPLIT waves share a row block, wave W updating A_ic blocks (W / SPLIT, (W % SPLIT) NIC + jj), jj < NIC = 4 / SPLIT,
+// beside its A_cc blocks: at most 7 / 5 / 4 blocks per wave for SPLIT = 1 / 2 / 4.
+template <int W, bool PANEL, int NR, int SPLIT>
 __device__ __forceinline__ void update_eager_wave(const double* __restrict__ Acc, const double* __restrict__ Aic,
                                                   const double* __restrict__ Lc, const double* __restrict__ Li,
                                                   int64_t lda, double* sA, double* sP, int c, int rowblk0,
                                                   const PotrfFwd& f, double* sZ, double* sR) {
   constexpr int NCC = W < 2 ? 3 : 2;
-  constexpr int NIC = HALF ? 2 : 4;             // A_ic blocks of this wave
-  constexpr int RB = HALF ? (W >> 1) : W;       // its A_ic row block (within the workgroup's rows)
-  constexpr int JB0 = HALF ? 2 * (W & 1) : 0;   // its first A_ic column block
-  constexpr int NRI = HALF ? 4 : 8;             // double2 loads of L_i per thread (32 or 64 rows)
-  constexpr bool FOLD_ROWS = !PANEL || !HALF || (W & 1) == 0;  // waves that fold their row block's right-hand side
+  constexpr int NIC = 4 / SPLIT;                 // A_ic blocks of this wave
+  constexpr int RB = W / SPLIT;                  // its A_ic row block (within the workgroup's rows)
+  constexpr int JB0 = (W % SPLIT) * NIC;         // its first A_ic column block
+  constexpr int NRI = 8 / SPLIT;                 // double2 loads of L_i per thread (64 / SPLIT rows)
+  constexpr bool FOLD_ROWS = !PANEL || (W % SPLIT) == 0;  // waves that fold their row block's right-hand side
   const int t = threadIdx.x, lane = t & 63;
   const int g = lane >> 4, cl = lane & 15;
   double2 rl[8], ri[NRI];
@@ -301,16 +302,16 @@ __device__ __forceinline__ void update_eager_wave(const double* __restrict__ Acc
   }
 }
 
-template <bool PANEL, int NR, bool HALF>
+template <bool PANEL, int NR, int SPLIT>
 __device__ __forceinline__ void update_eager(const double* __restrict__ Acc, const double* __restrict__ Aic,
                                              const double* __restrict__ Lc, const double* __restrict__ Li, int64_t lda,
                                              double* sA, double* sP, int c, int rowblk0, const PotrfFwd& f, double* sZ,
                                              double* sR) {
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {  // wave-uniform: compile-time block lists per wave
-    case 0: update_eager_wave<0, PANEL, NR, HALF>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
-    case 1: update_eager_wave<1, PANEL, NR, HALF>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
-    case 2: update_eager_wave<2, PANEL, NR, HALF>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
-    default: update_eager_wave<3, PANEL, NR, HALF>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
+    case 0: update_eager_wave<0, PANEL, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
+    case 1: update_eager_wave<1, PANEL, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
+    case 2: update_eager_wave<2, PANEL, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
+    default: update_eager_wave<3, PANEL, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
   }
 }
 
@@ -354,15 +355,15 @@ __device__ __forceinline__ void load_tile_lds(const double* __restrict__ G, int6
   }
 }
 
-// Panel workgroup p of block column c (see the file comment); NR > 0: with the forward fold (PotrfFwd).  HALF (p > 0):
-// the workgroup owns rows 32 h .. 32 h + 31 of row block c + p (a 96-row tall panel), so that its pre-update and its T /
-// U items are two thirds of a full one; the host splits the row blocks this way where the launch still fits the
-// co-resident slots (StepPlan::half).
-template <int NR, bool HALF>
+// Panel workgroup p of block column c (see the file comment); NR > 0: with the forward fold (PotrfFwd).  SPLIT > 1
+// (p > 0): the workgroup owns rows PROWS h .. PROWS h + PROWS - 1 (PROWS = 64 / SPLIT) of row block c + p, a
+// (64 + PROWS)-row tall panel, so that its pre-update MFMAs and its T / U items shrink with the split; the host picks the
+// largest split whose launch still fits the co-resident slots (StepPlan::split).
+template <int NR, int SPLIT>
 __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, int c, int p, int h, int nblk, int c0,
                                            double* __restrict__ Dinv, int32_t* __restrict__ info, double* lds,
                                            const PotrfFwd& f) {
-  constexpr int PROWS = HALF ? NB / 2 : NB;  // rows of A_ic this workgroup owns
+  constexpr int PROWS = NB / SPLIT;  // rows of A_ic this workgroup owns
   double* sA = lds;             // A_cc -> L_cc
   double* sP = sA + NB * LD64;  // A_ic -> L_ic (p > 0)
   double* sDb = sP + NB * LD64; // D_ss, double-buffered by step parity (2 x 16 x LDD)
@@ -379,7 +380,7 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
   static_assert(NB * GPX_MAX_RHS <= DBUF && 2 * NB * GPX_MAX_RHS + 3 * 16 * GPX_MAX_RHS <= NB * LD64, "fold LDS");
   const int nrow = panel ? 4 + PROWS / 16 : 4;  // 16-row blocks of the tall panel
   const int bi = c + p;
-  const int row0 = bi * NB + (HALF ? PROWS * h : 0);  // first global row of this workgroup's A_ic rows
+  const int row0 = bi * NB + PROWS * h;  // first global row of this workgroup's A_ic rows
   const double* Acc = A + (int64_t)c * NB * lda + (int64_t)c * NB;
   double* Aic = A + (int64_t)row0 * lda + (int64_t)c * NB;
   if (t == 0) s_tdone = 0;
@@ -392,13 +393,13 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
 #ifndef GPX_POTRF_TILE_PREUPDATE
     if (kk == NB) {
       if (panel)
-        update_eager<true, NR, HALF>(Acc, Aic, Lc, Li, lda, sA, sP, c, row0, f, sZ, sR);
+        update_eager<true, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, c, row0, f, sZ, sR);
       else
-        update_eager<false, NR, false>(Acc, Aic, Lc, Li, lda, sA, sP, c, c * NB, f, sZ, sR);
+        update_eager<false, NR, 1>(Acc, Aic, Lc, Li, lda, sA, sP, c, c * NB, f, sZ, sR);
     } else
 #endif
     {
-      // (never HALF: the host splits panels only in schedules whose panels apply one column)
+      // (never split: the host splits panels only in schedules whose panels apply one column)
       // (the host folds the forward substitution only into schedules whose panels apply one column: kk == NB)
       Tile64 tl;
       update_to_lds(tl, Acc, lda, Lc, Lc, lda, kk, smem, sA);
@@ -622,15 +623,15 @@ __device__ __forceinline__ void lookahead_role(double* __restrict__ A, int64_t l
 struct StepPlan {
   int npanel, nlook, ntrail, c0, look_a, cfirst, k0, flush;
   int tbase, xmap;  // first trailing workgroup (a multiple of 8 when xmap: XCD-chunked tile order), tile order
-  int half;         // panel row blocks c+1.. split into two 32-row workgroups (panel workgroup b > 0: p = 1 + (b-1)/2)
+  int split;        // panel row blocks c+1.. split into 1, 2 or 4 workgroups (panel workgroup b > 0: p = 1 + (b-1) / split)
 };
 
 // slots > 0: the co-resident workgroup slots a problem may fill (two per CU, shared by a batch); the panel row blocks are
-// split in halves (StepPlan::half) when the panels apply exactly one column and the split launch still fits them.
+// split in 2 (StepPlan::split) when the panels apply exactly one column and the split launch still fits the slots.
 inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush, int xmap = 0, int slots = 0) {
   StepPlan s;
   s.npanel = nblk - c;
-  s.half = 0;
+  s.split = 1;
   s.flush = flush ? 1 : 0;
   s.k0 = last_flush;
   if (mode == 0) {
@@ -650,11 +651,14 @@ inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush,
   s.xmap = xmap;
   const bool eager = mode == 1 || c == 0 || c - last_flush == 1;
   if (slots > 0 && eager && s.npanel > 1) {
-    const int np = 1 + 2 * (s.npanel - 1);
-    const int tb = xmap ? (np + s.nlook + 7) & ~7 : np + s.nlook;
-    if (tb + s.ntrail <= slots) {
-      s.half = 1;
-      s.npanel = np;
+    for (int sp = 2; sp >= 2; sp >>= 1) {  // split 4 measured slower at n = 4096 (potrf 1.48 vs 1.46 ms), equal below
+      const int np = 1 + sp * (s.npanel - 1);
+      const int tb = xmap ? (np + s.nlook + 7) & ~7 : np + s.nlook;
+      if (tb + s.ntrail <= slots) {
+        s.split = sp;
+        s.npanel = np;
+        break;
+      }
     }
   }
   s.tbase = xmap ? (s.npanel + s.nlook + 7) & ~7 : s.npanel + s.nlook;  // padding workgroups exit at once
@@ -682,10 +686,10 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, StepPlan
       f.r += blockIdx.y * f.sb;
       f.z += blockIdx.y * f.sb;
     }
-    if (s.half && b > 0)
-      panel_role<NR, true>(A, lda, c, 1 + ((b - 1) >> 1), (b - 1) & 1, nblk, s.c0, Dinv, info, lds, f);
+    if (s.split == 2 && b > 0)
+      panel_role<NR, 2>(A, lda, c, 1 + ((b - 1) >> 1), (b - 1) & 1, nblk, s.c0, Dinv, info, lds, f);
     else
-      panel_role<NR, false>(A, lda, c, b, 0, nblk, s.c0, Dinv, info, lds, f);
+      panel_role<NR, 1>(A, lda, c, b, 0, nblk, s.c0, Dinv, info, lds, f);
   } else if (role == 1)
     lookahead_role(A, lda, c, s.look_a, b - s.npanel, lds);
   else
@@ -766,7 +770,7 @@ static void for_each_step(const Context* ctx, int nblk, int mode, int cend, int 
 // Co-resident workgroup slots per problem (two per CU at the step kernel's LDS size, shared by the batch), or 0 when
 // the device cannot be queried (no half-panel split then).
 static int potrf_slots(Context* ctx, int batch) {
-#ifdef GPX_NO_HALF
+#ifdef GPX_NO_SPLIT
   return 0;
 #endif
   if (ctx->cu_count <= 0) {
