@@ -150,12 +150,8 @@ __device__ __forceinline__ double dbl_of(unsigned lo, unsigned hi) {
 }
 
 // (x_0 + x_2) + (x_1 + x_3) over the four 16-lane rows q of a wave, the same value in every row: gfx950's
-// v_permlane32_swap / v_permlane16_swap (VALU) instead of two ds_bpermute round trips.
+// v_permlane32_swap / v_permlane16_swap (VALU) instead of two ds_bpermute round trips (measured equal inside the fold).
 __device__ __forceinline__ double rowsum4(double x) {
-#ifdef GPX_FOLD_SHFL
-  x += __shfl_xor(x, 32);
-  return x + __shfl_xor(x, 16);
-#else
   const unsigned long long u = __double_as_longlong(x);
   const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)u, (unsigned)u, false, false);
   const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(u >> 32), (unsigned)(u >> 32), false, false);
@@ -164,7 +160,6 @@ __device__ __forceinline__ double rowsum4(double x) {
   const auto lo2 = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
   const auto hi2 = __builtin_amdgcn_permlane16_swap((unsigned)(v >> 32), (unsigned)(v >> 32), false, false);
   return dbl_of(lo2[0], hi2[0]) + dbl_of(lo2[1], hi2[1]);  // even row + odd row
-#endif
 }
 
 // One wave: out[rr] = sum_k M[a][k] v[k][rr] for the 16-row block M (LDS, row length ldm, KQ columns per lane
@@ -477,9 +472,7 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
         }
       }
       if constexpr (NR > 0) {
-#ifndef GPX_FOLD_NO_P0
         if (!panel) fwd_pivot_step<NR>(s, w, D, sA, sR, sZs, sZall);
-#endif
       }
     }
     GPX_PANEL_STAMP(3 + 3 * s);
@@ -770,7 +763,7 @@ static void for_each_step(const Context* ctx, int nblk, int mode, int cend, int 
 // Co-resident workgroup slots per problem (two per CU at the step kernel's LDS size, shared by the batch), or 0 when
 // the device cannot be queried (no half-panel split then).
 static int potrf_slots(Context* ctx, int batch) {
-#ifdef GPX_NO_SPLIT
+#ifdef GPX_NO_SPLIT  // A/B builds (tools/ab_multi.sh): the unsplit panels
   return 0;
 #endif
   if (ctx->cu_count <= 0) {
@@ -816,7 +809,7 @@ hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* 
     return e;
   }
   PotrfFwd f;
-#if !defined(GPX_POTRF_TILE_PREUPDATE) && !defined(GPX_NO_FOLD)
+#if !defined(GPX_POTRF_TILE_PREUPDATE) && !defined(GPX_NO_FOLD)  // GPX_NO_FOLD: A/B builds without the fold
   // the fold needs panels that apply exactly one pending column per launch (eager or lookahead schedules)
   if (fr && fr->Y && fr->buf && (potrf_mode(ctx, nblk) == 1 || potrf_lazy(ctx, nblk) == 1)) {
     const int64_t nr = rhs_row(fr->nrhs);
