@@ -46,7 +46,7 @@ int main(int argc, char** argv) {
     CK(hipMemset(info, 0, 4));
     for (int cc = 0; cc < c; ++cc) {
       const StepPlan s = plan(cc);
-      potrf_step_kernel<<<s.tbase + s.ntrail, WG>>>(A, n, cc, nblk, s, Dinv, info, 0, 0, 0, 0);
+      potrf_step_kernel<0><<<s.tbase + s.ntrail, WG>>>(A, n, cc, nblk, s, Dinv, info, 0, 0, 0, PotrfFwd());
     }
     CK(hipDeviceSynchronize());
     const StepPlan s = plan(c);
@@ -54,7 +54,7 @@ int main(int argc, char** argv) {
     const int first = mode == 2 ? s.tbase : 0;
     if (grid == 0) return 0.0f;
     CK(hipEventRecord(e0));
-    for (int i = 0; i < 20; ++i) potrf_step_kernel<<<grid, WG>>>(A, n, c, nblk, s, Dinv, info, first, 0, 0, 0);
+    for (int i = 0; i < 20; ++i) potrf_step_kernel<0><<<grid, WG>>>(A, n, c, nblk, s, Dinv, info, first, 0, 0, PotrfFwd());
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms;
