@@ -252,7 +252,7 @@ __global__ void __launch_bounds__(WG) mll_finalize_kernel(int n, int nrhs, const
   }
 }
 
-// k-chunk of the split.  n = 4096 (tools/mll_probe.hip): kc 512 / 1024 / 2048 / npad -> 0.670 / 0.620 / 0.678 /
+// k-chunk of the split.  n = 4096 (round-1 probe, profiles/r01_mll_kchunk_sweep.log): kc 512 / 1024 / 2048 / npad -> 0.670 / 0.620 / 0.678 /
 // 0.742 ms: a shallower chunk balances the deep tiles, but the dK epilogue runs once per unit; n = 8192
 // (tools/mll_kc_sweep.sh): 512 / 1024 / 2048 -> 5.33 / 4.74 / 4.65 ms; n = 16384: 2048 / 4096 / 8192 / 16384 ->
 // 28.0 / 27.1 / 26.2 / 26.1 ms (thousands of tiles balance themselves).

@@ -28,7 +28,7 @@
 #include "gpx_device.h"
 #include "gpx_chol64.h"
 
-// Optional timestamp hook for tools/potrf_bench.hip (compiled out in the library).
+// Optional timestamp hooks for tools/potrf_steps_probe.hip (compiled out in the library).
 #ifndef GPX_PANEL_STAMP
 #define GPX_PANEL_STAMP(i)
 #endif
