@@ -158,10 +158,6 @@ gpx_status gpx_destroy(gpx_handle h) {
     (void)hipEventDestroy(pt.stop);
   }
   for (auto ev : c->free_events) (void)hipEventDestroy(ev);
-  {
-    gpx::DeviceScope dev(c->device);
-    gpx::potrf_dag_release(c);
-  }
   delete c;
   return GPX_OK;
 }
@@ -176,7 +172,7 @@ gpx_status gpx_set_stream(gpx_handle h, void* stream) {
 static gpx_status set_option(Context* c, int32_t option, int64_t v) {
   switch (option) {
     case GPX_OPT_POTRF_SCHEDULE:
-      if (v < 0 || v > 2) return fail(c, GPX_INVALID_ARG, "potrf_schedule must be 0, 1 or 2");
+      if (v < 0 || v > 1) return fail(c, GPX_INVALID_ARG, "potrf_schedule must be 0 or 1");
       c->potrf_schedule = (int)v;
       return GPX_OK;
     case GPX_OPT_SPIN_LIMIT:

@@ -30,15 +30,16 @@ struct Context {
   int64_t timer_launches[GPX_TIMER_COUNT] = {0};
   std::vector<PendingTimer> pending;
   std::vector<hipEvent_t> free_events;
-  // persistent dataflow Cholesky (gpx_potrf_dag.hip): CU count, task-list cache, zeroed-per-call sync words
-  int cu_count = 0;
+  int cu_count = 0;  // CUs of the device (queried once: persistent solve grid, Cholesky slot budget)
+  // the diagnostic persistent dataflow Cholesky (tools/gpx_potrf_dag.hip, probe builds only): task-list cache and sync
+  // words; never allocated by the library itself
   void* dag_cache = nullptr;
   void* dag_sync = nullptr;
   size_t dag_sync_bytes = 0;
   // bounded spins of the in-launch hand-offs (potrf DAG, potrs): passes before a waiter gives up and reports a timeout
   unsigned spin_limit = 1u << 22;
   // options (include/gpx.h GPX_OPT_*; set by gpx_set_option or GPX_OPTIONS at gpx_create)
-  int potrf_schedule = 0;  // 0 by size (multi-launch: measured faster at every size), 1 multi-launch, 2 dataflow where it applies
+  int potrf_schedule = 0;  // 0 by size, 1 multi-launch (the same schedule; the dataflow one lives in tools/)
   int sweep_fused = 1;     // fused small-n sweep where it applies
   int gram_split = 0;      // 0 by size, else workgroups per Gram tile
   int potrf_lazy = 0;      // multi-launch flush interval, 0 by size
@@ -107,12 +108,6 @@ inline int rhs_row(int nrhs) { return nrhs == 1 ? 1 : GPX_MAX_RHS; }
 hipError_t launch_potrf(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info,
                         const Batch& bt = Batch(), double* W = nullptr, int64_t ldw = 0,
                         const ForwardRhs* fr = nullptr, bool* z_done = nullptr);
-// the persistent dataflow schedule for npad <= 4096 (gpx_potrf_dag.hip); launch_potrf uses it when
-// potrf_dag_workers() > 0
-int potrf_dag_workers(Context* c, int npad, int batch);
-hipError_t launch_potrf_dag(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info,
-                            const Batch& bt, double* W, int64_t ldw, const ForwardRhs* fr = nullptr);
-void potrf_dag_release(Context* c);
 hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, const double* Dinv, double* W,
                         int64_t ldw, double* T, const Batch& bt = Batch(), bool diag_done = false);
 hipError_t launch_alpha(Context* c, int n, int npad, const double* W, int64_t ldw, const double* Y, int64_t ldy,

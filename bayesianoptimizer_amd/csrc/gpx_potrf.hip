@@ -803,11 +803,6 @@ hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* 
   // the trailing tiles' write-through stores address a 128-row tile through a buffer descriptor (32-bit byte offsets)
   if (lda > (int64_t(1) << 20)) return hipErrorInvalidValue;
   if (z_done) *z_done = false;
-  if (ctx->potrf_schedule == 2 && potrf_dag_workers(ctx, npad, bt.count) > 0) {
-    hipError_t e = launch_potrf_dag(ctx, npad, A, lda, Dinv, info, bt, W, ldw, fr);
-    if (e == hipSuccess && z_done && fr && fr->Y) *z_done = true;
-    return e;
-  }
   PotrfFwd f;
 #if !defined(GPX_POTRF_TILE_PREUPDATE) && !defined(GPX_NO_FOLD)  // GPX_NO_FOLD: A/B builds without the fold
   // the fold needs panels that apply exactly one pending column per launch (eager or lookahead schedules)

@@ -133,9 +133,8 @@ size_t gpx_acq_params_size(void);
 /* Per-handle options (tuning and diagnostics; every default is the measured best).  gpx_create reads the environment
  * variable GPX_OPTIONS once ("name=value,name=value", names as below in lower case without the prefix, e.g.
  * "potrf_schedule=1,sweep_fused=0"); nothing else in the library reads the environment.
- *  GPX_OPT_POTRF_SCHEDULE  0 by size (default: one launch per block column at every size, measured faster than the
- *                          dataflow schedule), 1 multi-launch everywhere, 2 the persistent dataflow launch wherever it
- *                          applies (padded n <= 4096; diagnostic)
+ *  GPX_OPT_POTRF_SCHEDULE  0 by size (default), 1 one launch per block column everywhere (today the same schedule;
+ *                          the persistent dataflow variant, measured slower, is a probe build in tools/)
  *  GPX_OPT_SPIN_LIMIT      polls before an in-launch hand-off (Cholesky dataflow, triangular solve) gives up and
  *                          reports GPX_INFO_TIMEOUT (default 4194304; 0 = give up at the first unmet poll: tests)
  *  GPX_OPT_SWEEP_FUSED     1 (default) the fused small-n sweep where it applies (padded n <= 256), 0 the K* + trmm path

@@ -1,8 +1,9 @@
-"""The persistent dataflow Cholesky (gpx_potrf_dag.hip, opt-in: potrf_schedule = 2; measured slower than the default
-multi-launch schedule) against the multi-launch schedule and the oracle; failure reporting of the two persistent launches (dataflow Cholesky, triangular solve) when an
-in-launch hand-off times out; the per-handle options that replaced the library's environment knobs (include/gpx.h
-GPX_OPT_*).  Reference call sites: psd_safe_cholesky [upstream] reached from optimization/Bayesian.py:89-94, jitter
-retry optimization/Bayesian6.py:481-488."""
+"""Failure reporting of the persistent launches (the triangular solve's hand-offs) when an in-launch hand-off times
+out, the per-handle options that replaced the library's environment knobs (include/gpx.h GPX_OPT_*), the pivot of a
+failing factorisation deep in the matrix, batch invariance of the factor, and the leading-dimension limit.  (The
+persistent dataflow Cholesky these tests once compared against is a probe build in tools/gpx_potrf_dag.hip: measured
+slower than the multi-launch schedule)  Reference call sites: psd_safe_cholesky [upstream] reached from
+optimization/Bayesian.py:89-94, jitter retry optimization/Bayesian6.py:481-488."""
 import os
 
 import numpy as np
@@ -17,47 +18,13 @@ from tests.test_gpu_parity import RTOL, pair, t
 pytestmark = pytest.mark.gpu
 
 
-def _factor(engine, X, kp, n, schedule):
-    engine.set_option("potrf_schedule", schedule)
-    try:
-        K = engine.gram(t(X), kp)
-        Dinv, info = engine.potrf(K, n)
-        torch.cuda.synchronize()
-    finally:
-        engine.set_option("potrf_schedule", 0)
-    return np.tril(K.cpu().numpy()), Dinv.cpu().numpy(), int(info.item())
-
-
-@pytest.mark.parametrize("n,kind", [(1, "rbf"), (129, "matern52"), (256, "rbf"), (700, "scale_linear_matern52"),
-                                    (2048, "rbf"), (4096, "rbf")])
-def test_dataflow_factor_matches_multilaunch_and_oracle(engine, n, kind):
-    d = 8
-    X, _ = O.synthetic_problem(n, d, n + 11)
-    kp, op = pair(kind, d, noise=1e-4)
-    L2, D2, i2 = _factor(engine, X, kp, n, 2)
-    L1, D1, i1 = _factor(engine, X, kp, n, 1)
-    assert i1 == i2 == 0
-    npad = L2.shape[0]
-    scale = np.abs(L1).max()
-    # two arrangements of the same fp64 arithmetic (aggregated trailing products vs one column per launch)
-    assert np.abs(L2 - L1).max() <= 1e-12 * scale
-    np.testing.assert_array_equal(L2[n:, n:], np.eye(npad - n))
-    for b in range(npad // 64):
-        blk = L2[64 * b:64 * b + 64, 64 * b:64 * b + 64]
-        np.testing.assert_allclose(D2[b] @ blk, np.eye(64), atol=1e-10)
-    if n <= 2048:
-        Lr = O.cholesky(O.gram(X, op))
-        assert np.abs(L2[:n, :n] - Lr).max() <= RTOL * np.abs(Lr).max()
-
-
-def test_dataflow_not_pd_pivot_deep(engine):
-    # a pivot in the middle of a 4096 factor (chain step 32): the dataflow schedule stops there and reports it like the
-    # multi-launch schedule does
+def test_not_pd_pivot_deep(engine):
+    # a pivot in the middle of a 4096 factor (launch 32, split panels): the factorisation stops there and reports it
     n = 4096
     X, _ = O.synthetic_problem(n, 8, 5)
     kp, _ = pair("rbf", 8, noise=1e-4)
     piv = 2085
-    for schedule in (1, 2):
+    for schedule in (0, 1):
         engine.set_option("potrf_schedule", schedule)
         try:
             K = engine.gram(t(X), kp)
@@ -69,14 +36,13 @@ def test_dataflow_not_pd_pivot_deep(engine):
 
 
 def test_fit_timeout_raises_timeout_error_not_not_pd(engine):
-    """spin_limit = 0: every in-launch wait gives up at its first unmet poll.  Under both schedules the fit raises
-    GPXTimeoutError (dataflow: the pool tasks wait for the chain from the start; multi-launch: the backward solve's
-    hand-offs), never NotPositiveDefiniteError (a jitter retry would not cure it), and the next call with the default
-    limit is correct again."""
+    """spin_limit = 0: every in-launch wait gives up at its first unmet poll.  The fit raises GPXTimeoutError (the
+    backward solve's hand-offs), never NotPositiveDefiniteError (a jitter retry would not cure it), and the next call
+    with the default limit is correct again."""
     n = 4096
     X, y = O.synthetic_problem(n, 8, 21)
     kp, _ = pair("rbf", 8, noise=1e-4)
-    for schedule in (0, 2):
+    for schedule in (0, 1):
         engine.set_option("potrf_schedule", schedule)
         engine.set_option("spin_limit", 0)
         try:
@@ -125,14 +91,14 @@ def test_batched_timeout_names_the_problem(engine):
 
 
 def test_options_roundtrip_and_validation(engine):
-    for name, value in (("potrf_schedule", 2), ("spin_limit", 12345), ("sweep_fused", 0), ("gram_split", 2),
+    for name, value in (("potrf_schedule", 1), ("spin_limit", 12345), ("sweep_fused", 0), ("gram_split", 2),
                         ("potrf_lazy", 3), ("potrf_mode", 1)):
         old = engine.get_option(name)
         engine.set_option(name, value)
         assert engine.get_option(name) == value
         engine.set_option(name, old)
         assert engine.get_option(name) == old
-    for name, bad in (("potrf_schedule", 3), ("spin_limit", -1), ("sweep_fused", 2), ("gram_split", 3),
+    for name, bad in (("potrf_schedule", 2), ("spin_limit", -1), ("sweep_fused", 2), ("gram_split", 3),
                       ("potrf_lazy", 17), ("potrf_mode", 2)):
         with pytest.raises(GPXError) as e:
             engine.set_option(name, bad)
@@ -153,12 +119,13 @@ def test_options_from_environment_at_create():
 
 
 def test_fit_results_identical_across_pool_sizes(engine):
-    """The dataflow schedule decides who runs a task, never how: a batched fit (64 workgroups per problem) equals the
-    single fit (256 workgroups) bit for bit at n = 4096; so does the default multi-launch schedule."""
+    """The schedule decides who runs a piece of work (the panel split depends on the co-resident slots a problem gets,
+    which a batch shares), never how a factor entry is computed: a batched fit of four problems equals the single fit
+    bit for bit at n = 4096."""
     n = 4096
     X, y = O.synthetic_problem(n, 8, 40)
     kp, _ = pair("rbf", 8, noise=1e-4)
-    for schedule in (2, 0):
+    for schedule in (0,):
         engine.set_option("potrf_schedule", schedule)
         try:
             st = engine.fit(t(X), t(y), kp)

@@ -1,4 +1,6 @@
 // Persistent dataflow Cholesky (lower, NB = 64) for npad <= 4096: ONE launch per factorisation (per batch).
+// DIAGNOSTIC PROBE BUILD ONLY (tools/dag_probe.hip): measured slower than the library's multi-launch schedule at every
+// size, so it is not part of libgpx.
 // SURVEY §8a row a4 (psd_safe_cholesky in GPyTorch's exact path [upstream], reached from
 // optimization/Bayesian.py:89-94); the failing pivot is reported in *info for the jitter retry of
 // optimization/Bayesian6.py:481-488.
@@ -47,6 +49,12 @@
 #endif
 
 namespace gpx {
+// entry points of this probe build (not part of libgpx)
+int potrf_dag_workers(Context* c, int npad, int batch);
+hipError_t launch_potrf_dag(Context* c, int npad, double* A, int64_t lda, double* Dinv, int32_t* info,
+                            const Batch& bt, double* W, int64_t ldw, const ForwardRhs* fr = nullptr);
+void potrf_dag_release(Context* c);
+
 namespace dag {
 
 constexpr int LD = LD64;              // LDS row length of a 64x64 tile (doubles)
