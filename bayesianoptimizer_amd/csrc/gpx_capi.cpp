@@ -171,10 +171,6 @@ gpx_status gpx_set_stream(gpx_handle h, void* stream) {
 
 static gpx_status set_option(Context* c, int32_t option, int64_t v) {
   switch (option) {
-    case GPX_OPT_POTRF_SCHEDULE:
-      if (v < 0 || v > 1) return fail(c, GPX_INVALID_ARG, "potrf_schedule must be 0 or 1");
-      c->potrf_schedule = (int)v;
-      return GPX_OK;
     case GPX_OPT_SPIN_LIMIT:
       if (v < 0 || v > 0x7fffffff) return fail(c, GPX_INVALID_ARG, "spin_limit must be in [0, 2^31)");
       c->spin_limit = (unsigned)v;
@@ -201,8 +197,7 @@ static gpx_status set_option(Context* c, int32_t option, int64_t v) {
 }
 
 static int option_by_name(const std::string& name) {
-  static const char* names[GPX_OPT_COUNT] = {"potrf_schedule", "spin_limit", "sweep_fused",
-                                             "gram_split",     "potrf_lazy", "potrf_mode"};
+  static const char* names[GPX_OPT_COUNT] = {"spin_limit", "sweep_fused", "gram_split", "potrf_lazy", "potrf_mode"};
   for (int i = 0; i < GPX_OPT_COUNT; ++i)
     if (name == names[i]) return i;
   return -1;
@@ -239,7 +234,6 @@ gpx_status gpx_get_option(gpx_handle h, int32_t option, int64_t* value_host) {
   if (!c) return GPX_INVALID_ARG;
   GPX_NONNULL(c, value_host);
   switch (option) {
-    case GPX_OPT_POTRF_SCHEDULE: *value_host = c->potrf_schedule; return GPX_OK;
     case GPX_OPT_SPIN_LIMIT: *value_host = c->spin_limit; return GPX_OK;
     case GPX_OPT_SWEEP_FUSED: *value_host = c->sweep_fused; return GPX_OK;
     case GPX_OPT_GRAM_SPLIT: *value_host = c->gram_split; return GPX_OK;

@@ -71,36 +71,6 @@ __device__ __forceinline__ double xrow_bcast_f64(double v) {
   return __longlong_as_double(((unsigned long long)hi << 32) | lo);
 }
 
-// Pivot J of the 16x16 block: rows r > J get A[r][c] -= A[r][J] A[J][c] / A[J][J], row J of X is scaled by
-// A[J][J]^{-1/2} and X's rows r > J get the same row operation; rows < J are left untouched.  Row J of A and of X
-// (the lane's own four columns) come from lane J of the same 16-lane DPP row (row_newbcast:J); A[r][J] lives in DPP
-// row J/4 and comes by two permlane swaps (xrow_bcast_f64).  Measured per pivot: 306 cycles with 64-bit DPP moves,
-// 390 with a wave-local LDS broadcast slot (two ds_read_b128 per row, a write -> read round trip on the chain), ~380
-// with ds_bpermute for A[r][J].
-template <int J>
-__device__ __forceinline__ void chol16_pivot(Blk16& b, int r, int g, int& fail) {
-  constexpr int GJ = J >> 2, QJ = J & 3;
-  const double piv = readlane_f64(b.a[QJ], J + 16 * GJ);
-  const double arj = xrow_bcast_f64<GJ>(b.a[QJ]);  // A[r][J]
-  double aj[4], xj[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    aj[q] = row_bcast<J>(b.a[q]);
-    xj[q] = row_bcast<J>(b.x[q]);
-  }
-  if (!(piv > 0.0) && fail < 0) fail = J;
-  const double isq = pivot_rsq(piv);
-  const double rinv = isq * isq;
-  const double coef = (r > J) ? -arj * rinv : 0.0;
-  const double coefx = (r == J) ? isq - 1.0 : coef;
-  if (g == GJ) b.l[QJ] = (r >= J) ? b.a[QJ] * isq : 0.0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    b.a[q] = fma(coef, aj[q], b.a[q]);
-    b.x[q] = fma(coefx, xj[q], b.x[q]);
-  }
-}
-
 // a[q] += ca * bcast_J(a[q]) and x[q] += cx * bcast_J(x[q]) (q = 0..3) as eight v_fmac_f64_dpp row_newbcast:J: the
 // gfx90a+ 64-bit DPP form folds the row broadcast into the FMA (hipcc emits v_mov_b64_dpp + v_fmac_f64 instead, three
 // instructions per value with the 32-bit halves).  The compiler's hazard recognizer does not see inside the asm, so
@@ -130,22 +100,6 @@ __device__ __forceinline__ void fmac_row_bcast8(double (&a)[4], double (&x)[4], 
   }
 }
 #undef GPX_FMAC_DPP8
-
-// chol16_pivot with the row broadcasts folded into the FMAs (fmac_row_bcast8): same arithmetic, same rounding (the
-// broadcast value is the pre-update A[J][c] / X[J][c], as in chol16_pivot).
-template <int J>
-__device__ __forceinline__ void chol16_pivot_fused(Blk16& b, int r, int g, int& fail) {
-  constexpr int GJ = J >> 2, QJ = J & 3;
-  const double piv = readlane_f64(b.a[QJ], J + 16 * GJ);
-  const double arj = xrow_bcast_f64<GJ>(b.a[QJ]);  // A[r][J]
-  if (!(piv > 0.0) && fail < 0) fail = J;
-  const double isq = pivot_rsq(piv);
-  const double rinv = isq * isq;
-  const double coef = (r > J) ? -arj * rinv : 0.0;
-  const double coefx = (r == J) ? isq - 1.0 : coef;
-  if (g == GJ) b.l[QJ] = (r >= J) ? b.a[QJ] * isq : 0.0;
-  fmac_row_bcast8<J>(b.a, b.x, coef, coefx);
-}
 
 // Pipelined pivot J in two asm blocks: (1) the register the next pivot reads, a[QN] (leading/trailing pads: its DPP
 // source may be fresh, and v_readlane / permlane read its result next); (2) the other three a[q] and the four x[q] (their
@@ -216,15 +170,10 @@ __device__ __forceinline__ void chol16_pivot_pipe(Blk16& b, int r, int g, int& f
 
 template <int... J>
 __device__ __forceinline__ void chol16_pivots(Blk16& b, int r, int g, int& fail, std::integer_sequence<int, J...>) {
-#if !defined(GPX_CHOL16_NOPIPE) && !defined(GPX_CHOL16_UNFUSED)
-  // tools/chol16_probe: 3632 vs 3937 cycles per 16-pivot block unpipelined (potrf n = 4096 1.756 vs 1.767 ms)
+  // software-pipelined across pivots: 3632 vs 3937 cycles per 16-pivot block unpipelined (round 2, tools/chol16_probe;
+  // potrf n = 4096 1.756 vs 1.767 ms); the row broadcasts folded into the FMAs: 306 vs 390 cycles per pivot
   double piv = readlane_f64(b.a[0], 0), arj = xrow_bcast_f64<0>(b.a[0]);
   (chol16_pivot_pipe<J>(b, r, g, fail, piv, arj), ...);
-#elif !defined(GPX_CHOL16_UNFUSED)
-  (chol16_pivot_fused<J>(b, r, g, fail), ...);
-#else
-  (chol16_pivot<J>(b, r, g, fail), ...);
-#endif
 }
 
 // Factor + invert the 16x16 SPD block at (o, o) of the LDS tile sA (both triangles present, symmetric) with one
@@ -250,155 +199,6 @@ __device__ __forceinline__ int chol16(double* sA, double* sD, int o) {
     sD[r * LDD + c] = (c <= r) ? b.x[q] : 0.0;
   }
   return fail;
-}
-
-// ---- 4-pivot blocked variant on the MFMA accumulator layout ----------------------------------------------------
-// The 16x16 block lives in the C/D layout of v_mfma_f64_16x16x4: lane (g = lane/16, col = lane%16) holds rows g + 4q
-// (q = 0..3) of column col, i.e. register q holds block row q (rows 4q .. 4q+3).  Step k factors pivots 4k .. 4k+3:
-//   1. the 4x4 diagonal block (10 values, v_readlane) is factored and inverted by every lane (uniform scalar chain:
-//      four rsq pivots + ~20 dependent FMAs), D_k = L_kk^{-1};
-//   2. X's block row k (X = L^{-1}, built from I by the same block row operations) becomes D_k X_k (cross-row
-//      broadcasts by permlane swaps, off the factorisation chain);
-//   3. the rows below get L_ik = A_ik D_k^T (the four columns of a row sit in one DPP quad: quad_perm broadcasts);
-//   4. the rank-4 trailing update A -= L_k L_k^T and X -= L_k X_k are ONE v_mfma_f64_16x16x4 each: their A operand is
-//      lane (kk, m) = -L[m][4k+kk] (rows <= 4k+3 zeroed), the trailing update's B operand the same register un-negated
-//      (lane (kk, n) = L[n][4k+kk]) and X's B operand X's own register k (lane (kk, n) = X[4k+kk][n]).  The operand
-//      register is gathered from the TRSM's lanes by ds_bpermute.
-// Per pivot ~150 cycles on the chain instead of ~380 for the rank-1 elimination above (chol16), whose per-pivot row
-// broadcasts dominate.
-template <int M>
-__device__ __forceinline__ double quad_bcast_f64(double v) {
-  const unsigned long long u = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_mov_dpp((int)(u & 0xffffffffull), M * 0x55, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), M * 0x55, 0xf, 0xf, false);
-  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
-}
-
-__device__ __forceinline__ double bpermute_f64(int src_lane, double v) {
-  const unsigned long long u = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_ds_bpermute(src_lane * 4, (int)(u & 0xffffffffull));
-  const int hi = __builtin_amdgcn_ds_bpermute(src_lane * 4, (int)(u >> 32));
-  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
-}
-
-__device__ __forceinline__ double sel4(int i, double v0, double v1, double v2, double v3) {
-  return i == 0 ? v0 : (i == 1 ? v1 : (i == 2 ? v2 : v3));
-}
-
-// sF: per step k, 32 doubles of wave-private LDS: L_kk then D_k = L_kk^{-1}, each 4x4 row-major (zeros above the
-// diagonal).  Lanes fetch their lane-dependent coefficients from it (one ds_read_b128 pair) instead of selecting
-// among the uniform values (v_cndmask chains were ~15 % of the first version's instructions).
-template <int K>
-__device__ __forceinline__ void chol16_block_step(d4& A, d4& X, int g, int col, unsigned& bad, double* sF) {
-  const int lane = threadIdx.x & 63;
-  // 1. the 4x4 diagonal block, uniform (v_readlane into SGPRs)
-  const double a00 = readlane_f64(A[K], 4 * K), a10 = readlane_f64(A[K], 16 + 4 * K),
-               a11 = readlane_f64(A[K], 16 + 4 * K + 1), a20 = readlane_f64(A[K], 32 + 4 * K),
-               a21 = readlane_f64(A[K], 32 + 4 * K + 1), a22 = readlane_f64(A[K], 32 + 4 * K + 2),
-               a30 = readlane_f64(A[K], 48 + 4 * K), a31 = readlane_f64(A[K], 48 + 4 * K + 1),
-               a32 = readlane_f64(A[K], 48 + 4 * K + 2), a33 = readlane_f64(A[K], 48 + 4 * K + 3);
-  const double r0 = pivot_rsq(a00);
-  const double l00 = a00 * r0, l10 = a10 * r0, l20 = a20 * r0, l30 = a30 * r0;
-  const double p1 = fma(-l10, l10, a11);
-  const double r1 = pivot_rsq(p1);
-  const double l11 = p1 * r1, l21 = fma(-l20, l10, a21) * r1, l31 = fma(-l30, l10, a31) * r1;
-  const double p2 = fma(-l21, l21, fma(-l20, l20, a22));
-  const double r2 = pivot_rsq(p2);
-  const double l22 = p2 * r2, l32 = fma(-l31, l21, fma(-l30, l20, a32)) * r2;
-  const double p3 = fma(-l32, l32, fma(-l31, l31, fma(-l30, l30, a33)));
-  const double r3 = pivot_rsq(p3);
-  const double l33 = p3 * r3;
-  // failed pivots as bits 4k + i (branch-free: the values are uniform but the compiler cannot prove it)
-  bad |= ((a00 > 0.0) ? 0u : 1u) << (4 * K) | ((p1 > 0.0) ? 0u : 2u) << (4 * K) | ((p2 > 0.0) ? 0u : 4u) << (4 * K) |
-         ((p3 > 0.0) ? 0u : 8u) << (4 * K);
-  // D_k = L_kk^{-1} (lower)
-  const double d10 = -(l10 * r0) * r1, d21 = -(l21 * r1) * r2, d32 = -(l32 * r2) * r3;
-  const double d20 = -fma(l21, d10, l20 * r0) * r2;
-  const double d31 = -fma(l32, d21, l31 * r1) * r3;
-  const double d30 = -fma(l32, d20, fma(l31, d10, l30 * r0)) * r3;
-  double* F = sF + 32 * K;
-  if (lane == 0) {
-    double2* F2 = reinterpret_cast<double2*>(F);
-    F2[0] = make_double2(l00, 0.0);
-    F2[1] = make_double2(0.0, 0.0);
-    F2[2] = make_double2(l10, l11);
-    F2[3] = make_double2(0.0, 0.0);
-    F2[4] = make_double2(l20, l21);
-    F2[5] = make_double2(l22, 0.0);
-    F2[6] = make_double2(l30, l31);
-    F2[7] = make_double2(l32, l33);
-    F2[8] = make_double2(r0, 0.0);
-    F2[9] = make_double2(0.0, 0.0);
-    F2[10] = make_double2(d10, r1);
-    F2[11] = make_double2(0.0, 0.0);
-    F2[12] = make_double2(d20, d21);
-    F2[13] = make_double2(r2, 0.0);
-    F2[14] = make_double2(d30, d31);
-    F2[15] = make_double2(d32, r3);
-  }
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): lane 0's table writes land before the wave reads them
-  const double* Dk = F + 16;
-  const int m = lane & 15, kk = lane >> 4;  // MFMA A/B operand coordinates of this lane
-  // 2. X block row k <- D_k X_k as one MFMA: A = D_k in rows 4k..4k+3 (lane (kk, m): D_k[m - 4k][kk]), B = X_k (X's own
-  //    register k), C = X with block row k cleared (its register k)
-  {
-    const double dop = (m >> 2) == K ? Dk[(m & 3) * 4 + kk] : 0.0;
-    d4 Xc = X;
-    Xc[K] = 0.0;
-    X = mfma16x16x4(dop, X[K], Xc);
-  }
-  const int cb = col >> 2, j = col & 3;
-  if constexpr (K < 3) {
-    // 3. L_ik = A_ik D_k^T for the block rows i > k (lanes col = 4k + j): coefficients D_k[j][0..3]
-    const double2 e01 = *reinterpret_cast<const double2*>(Dk + 4 * j);
-    const double2 e23 = *reinterpret_cast<const double2*>(Dk + 4 * j + 2);
-#pragma unroll
-    for (int i = K + 1; i < 4; ++i) {
-      const double v0 = quad_bcast_f64<0>(A[i]), v1 = quad_bcast_f64<1>(A[i]), v2 = quad_bcast_f64<2>(A[i]),
-                   v3 = quad_bcast_f64<3>(A[i]);
-      const double l = fma(e23.y, v3, fma(e23.x, v2, fma(e01.y, v1, e01.x * v0)));
-      A[i] = cb == K ? l : A[i];
-    }
-    // 4. operand lane (kk, m) = L[m][4k+kk] for m > 4k+3: from lane 16 (m%4) + 4k + kk, register m/4
-    const int src = 16 * (m & 3) + 4 * K + kk;
-    double op = 0.0;
-#pragma unroll
-    for (int i = K + 1; i < 4; ++i) {
-      const double v = bpermute_f64(src, A[i]);
-      op = (m >> 2) == i ? v : op;
-    }
-    A = mfma16x16x4(-op, op, A);
-    X = mfma16x16x4(-op, X[K], X);
-  }
-}
-
-// Factor + invert the 16x16 SPD block at (o, o) of sA with one wave, as chol16 (same outputs, same contract); sF: 128
-// doubles of LDS scratch for this wave.
-template <int LDD>
-__device__ __forceinline__ int chol16_mfma(double* sA, double* sD, int o, double* sF) {
-  const int lane = threadIdx.x & 63;
-  const int g = lane >> 4, col = lane & 15;
-  d4 A, X;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    A[q] = sA[(o + g + 4 * q) * LD64 + o + col];
-    X[q] = (g + 4 * q == col) ? 1.0 : 0.0;
-  }
-  unsigned bad = 0;
-  chol16_block_step<0>(A, X, g, col, bad, sF);
-  chol16_block_step<1>(A, X, g, col, bad, sF);
-  chol16_block_step<2>(A, X, g, col, bad, sF);
-  chol16_block_step<3>(A, X, g, col, bad, sF);
-  const int cb = col >> 2, j = col & 3;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int r = g + 4 * q;
-    // diagonal 4x4 blocks from the step tables, the rest from the TRSM'd registers
-    const double lv = cb == q ? sF[32 * q + 4 * g + j] : A[q];
-    sA[(o + r) * LD64 + o + col] = col <= r ? lv : 0.0;
-    sD[r * LDD + col] = col <= r ? X[q] : 0.0;
-  }
-  return bad ? __builtin_ctz(bad) : -1;
 }
 
 // X = L^{-1} of the lower-triangular 16x16 block at (o, o) of sL (already factored), by one wave: forward

@@ -31,15 +31,9 @@ struct Context {
   std::vector<PendingTimer> pending;
   std::vector<hipEvent_t> free_events;
   int cu_count = 0;  // CUs of the device (queried once: persistent solve grid, Cholesky slot budget)
-  // the diagnostic persistent dataflow Cholesky (tools/gpx_potrf_dag.hip, probe builds only): task-list cache and sync
-  // words; never allocated by the library itself
-  void* dag_cache = nullptr;
-  void* dag_sync = nullptr;
-  size_t dag_sync_bytes = 0;
-  // bounded spins of the in-launch hand-offs (potrf DAG, potrs): passes before a waiter gives up and reports a timeout
+  // bounded spins of the in-launch hand-offs (potrs): passes before a waiter gives up and reports a timeout
   unsigned spin_limit = 1u << 22;
   // options (include/gpx.h GPX_OPT_*; set by gpx_set_option or GPX_OPTIONS at gpx_create)
-  int potrf_schedule = 0;  // 0 by size, 1 multi-launch (the same schedule; the dataflow one lives in tools/)
   int sweep_fused = 1;     // fused small-n sweep where it applies
   int gram_split = 0;      // 0 by size, else workgroups per Gram tile
   int potrf_lazy = 0;      // multi-launch flush interval, 0 by size

@@ -48,8 +48,8 @@ using Tile128 = MfmaTile<2 * NB, 2 * NB, 16, false, false>;  // trailing update
 // Panel: sA, sP (64 x LD64 each) and the two D_ss buffers (16 x LDD); the Tile64 staging of the panel-side
 // update aliases sP + the D buffers (both written only after the update GEMMs).
 constexpr int LDD = 20;
-constexpr int DBUF = 768;  // >= 2 * 16 * LDD (+ 128 of chol16_mfma's factor tables), and sP + D buffers hold Tile64::LDS_DOUBLES
-static_assert(NB * LD64 + DBUF >= Tile64::LDS_DOUBLES && DBUF >= 2 * 16 * LDD + 128, "panel LDS aliasing");
+constexpr int DBUF = 768;  // >= 2 * 16 * LDD, and sP + D buffers hold Tile64::LDS_DOUBLES
+static_assert(NB * LD64 + DBUF >= Tile64::LDS_DOUBLES && DBUF >= 2 * 16 * LDD, "panel LDS aliasing");
 // + the forward fold's right-hand sides of a p > 0 panel workgroup (64 x GPX_MAX_RHS, stored at the workgroup's end:
 // a global store before a barrier would hold the barrier until it completes)
 constexpr int PANEL_LDS = 2 * NB * LD64 + DBUF + NB * GPX_MAX_RHS;
@@ -385,15 +385,12 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
     const int kk = (c - c0) * NB;
     const double* Lc = A + (int64_t)c * NB * lda + (int64_t)c0 * NB;
     const double* Li = A + (int64_t)row0 * lda + (int64_t)c0 * NB;
-#ifndef GPX_POTRF_TILE_PREUPDATE
     if (kk == NB) {
       if (panel)
         update_eager<true, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, c, row0, f, sZ, sR);
       else
         update_eager<false, NR, 1>(Acc, Aic, Lc, Li, lda, sA, sP, c, c * NB, f, sZ, sR);
-    } else
-#endif
-    {
+    } else {
       // (never split: the host splits panels only in schedules whose panels apply one column)
       // (the host folds the forward substitution only into schedules whose panels apply one column: kk == NB)
       Tile64 tl;
@@ -437,14 +434,9 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
     const int o = 16 * s;
     double* D = sDb + (s & 1) * 16 * LDD;
     if (w == 0) {
-#ifndef GPX_CHOL16_MFMA
+      // (4-pivot blocks on v_mfma_f64_16x16x4, tools/chol16_probe.hip: correct, but measured slower inside the panel,
+      // potrf 1.89 vs 1.76 ms at n = 4096: ~75 instructions per pivot and MFMA / ds_bpermute latency on the chain)
       const int f = chol16<LDD>(sA, D, o);
-#else
-      // 4-pivot blocks on v_mfma_f64_16x16x4 (gpx_chol64.h): correct, but measured slower inside the panel (potrf
-      // 1.89 vs 1.76 ms at n = 4096): like the rank-1 form it issues ~75 instructions per pivot (selects of the
-      // uniform 4x4 factors, cross-row broadcasts) and exposes MFMA / ds_bpermute latency on the chain
-      const int f = chol16_mfma<LDD>(sA, D, o, sDb + 2 * 16 * LDD);
-#endif
       if (f >= 0 && fail < 0) fail = o + f;
     }
     GPX_PANEL_STAMP(1 + 3 * s);
@@ -763,9 +755,6 @@ static void for_each_step(const Context* ctx, int nblk, int mode, int cend, int 
 // Co-resident workgroup slots per problem (two per CU at the step kernel's LDS size, shared by the batch), or 0 when
 // the device cannot be queried (no half-panel split then).
 static int potrf_slots(Context* ctx, int batch) {
-#ifdef GPX_NO_SPLIT  // A/B builds (tools/ab_multi.sh): the unsplit panels
-  return 0;
-#endif
   if (ctx->cu_count <= 0) {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -804,7 +793,6 @@ hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* 
   if (lda > (int64_t(1) << 20)) return hipErrorInvalidValue;
   if (z_done) *z_done = false;
   PotrfFwd f;
-#if !defined(GPX_POTRF_TILE_PREUPDATE) && !defined(GPX_NO_FOLD)  // GPX_NO_FOLD: A/B builds without the fold
   // the fold needs panels that apply exactly one pending column per launch (eager or lookahead schedules)
   if (fr && fr->Y && fr->buf && (potrf_mode(ctx, nblk) == 1 || potrf_lazy(ctx, nblk) == 1)) {
     const int64_t nr = rhs_row(fr->nrhs);
@@ -818,7 +806,6 @@ hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* 
     f.n = fr->n;
     f.mean = fr->mean;
   }
-#endif
   launch_steps(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, f);
   launch_dinv(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, W, ldw);
   const hipError_t e = hipGetLastError();

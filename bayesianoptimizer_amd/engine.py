@@ -202,7 +202,7 @@ class GPEngine:
 
     # -- fit --------------------------------------------------------------------------------------
     def set_option(self, name: str, value: int) -> None:
-        """Per-handle tuning / diagnostic option (include/gpx.h GPX_OPT_*: potrf_schedule, spin_limit, sweep_fused,
+        """Per-handle tuning / diagnostic option (include/gpx.h GPX_OPT_*: spin_limit, sweep_fused,
         gram_split, potrf_lazy, potrf_mode)."""
         self._check(self.lib.gpx_set_option(self.handle, _capi.OPTIONS[name], int(value)))
 
@@ -314,7 +314,9 @@ class GPEngine:
         return states
 
     def potrs(self, state: GPState, Y) -> torch.Tensor:
-        """alpha = K^{-1}(Y - const_mean) from the state's factor alone (gpx_potrs_f64): new targets on the same X."""
+        """alpha = K^{-1}(Y - const_mean) from the state's factor alone (gpx_potrs_f64): new targets on the same X.
+        The solve reports into an info word of its own (a copy of the state's): a timed-out hand-off raises
+        GPXTimeoutError here and leaves the fitted state (its L, alpha and info) valid."""
         Y = self._as_f64(Y, "Y")
         if Y.shape[0] != state.n:
             raise ValueError(f"Y must have {state.n} rows, got {Y.shape[0]}")
@@ -324,9 +326,12 @@ class GPEngine:
         self._check(self.lib.gpx_potrs_workspace_size(state.n, nrhs, ctypes.byref(nbytes)))
         ws = self.workspace("potrs", nbytes.value)
         self._bind_stream()
+        info = state.info.clone()
         self._check(self.lib.gpx_potrs_f64(
             self.handle, state.n, _ptr(state.L), state.L.stride(0), _ptr(state.Dinv), _ptr(Y), Y.stride(0), nrhs,
-            float(state.params.const_mean), _ptr(alpha), _ptr(state.info), _ptr(ws), ws.numel()))
+            float(state.params.const_mean), _ptr(alpha), _ptr(info), _ptr(ws), ws.numel()))
+        if int(info.item()) == _capi.GPX_INFO_TIMEOUT:
+            raise _capi.GPXTimeoutError("triangular solve hand-off timed out (GPX_OPT_SPIN_LIMIT)")
         return alpha
 
     def append(self, state: GPState, X, Y, check: bool = True, growth: float = 1.5) -> GPState:

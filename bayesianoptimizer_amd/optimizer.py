@@ -70,11 +70,16 @@ class GPConfig:
     # with fixed hyperparameters: freeze the input standardisation at the first fit and fold each round's new rows in
     # with the O(n^2 q) bordered update (gpx_append_f64) instead of refitting (Bayesian7.py:639 refits every round)
     incremental_updates: bool = True
-    # Above svgp_threshold training points (where the reference switches to SVGP: optimization/Bayesian6.py:589-596,
-    # scripts/run_optimization.py:40) the drop-in keeps the EXACT posterior over all points but stops paying O(n^3) per
-    # round: hyperparameters are fitted by marginal likelihood on a random subsample of svgp_threshold points and then
-    # held, and each round's new rows are folded in by the bordered update (O(n^2 q)).  The factor is rebuilt (and the
-    # hyperparameters refitted on a fresh subsample) whenever n has grown by this factor since the last rebuild.
+    # Opt-in large-n policy (off by default: every round is then a full exact refit over all n points, whatever n, as
+    # the reference refits its surrogate every round, Bayesian7.py:639; its svgp_threshold is accepted for
+    # compatibility, Bayesian7.py:207).  With large_n_policy=True, above svgp_threshold training points (where
+    # Bayesian6 switches to SVGP: optimization/Bayesian6.py:589-596, scripts/run_optimization.py:40) the drop-in keeps
+    # the EXACT posterior over all points but stops paying O(n^3) per round: hyperparameters are fitted by marginal
+    # likelihood on a random subsample of svgp_threshold points (drawn from an RNG of its own, so the candidate draws
+    # of the run are unchanged) and then held, and each round's new rows are folded in by the bordered update
+    # (O(n^2 q)).  The factor is rebuilt (and the hyperparameters refitted on a fresh subsample) whenever n has grown by
+    # large_n_refit_growth since the last rebuild, or would outgrow the factor's reserved capacity.
+    large_n_policy: bool = False
     large_n_refit_growth: float = 2.0
     # device memory the exact factor may take (L and W = L^{-T}: 2 n^2 doubles at capacity), as a fraction of the free
     # device memory at the rebuild; beyond it the run stops with a clear error instead of an allocator failure
@@ -155,7 +160,7 @@ class BayesianOptimizer:
         n_batches: int,
         batch_size: int,
         num_outputs: int = 8,
-        svgp_threshold: int = 3000,  # run_optimization.py:40's value; the large-n policy of GPConfig above it
+        svgp_threshold: int = 3000,  # run_optimization.py:40's value; GPConfig.large_n_policy (opt-in) above it
         resume: bool = False,
         target_total: Optional[int] = None,
         device: Optional[torch.device] = None,
@@ -184,6 +189,8 @@ class BayesianOptimizer:
             raise ValueError(f"unknown acquisition '{self.acquisition}'")
         self.seed = kwargs.get("seed", None)
         self._rng = np.random.default_rng(self.seed)
+        # the large-n policy's hyperparameter subsamples draw from their own stream (never shift the candidate draws)
+        self._subsample_rng = np.random.default_rng(None if self.seed is None else [int(self.seed), 1])
 
         self.table = _ResultsTable(output_dir, self.dim, self.num_outputs)
         self.results_csv_path, self.val_log_path = self.table.path, self.table.metrics_path
@@ -253,16 +260,17 @@ class BayesianOptimizer:
     def fit_gp_model(self):
         """Log-standardise (Bayesian7.py:363-385) and build the exact posterior for all outputs on the engine.
 
-        n <= svgp_threshold: a fresh fit each round (hyperparameters by marginal likelihood, or fixed), or - fixed
-        hyperparameters, incremental mode - the previous round's factor extended by the rows observed since.
-        n > svgp_threshold (the reference's SVGP switch, Bayesian6.py:589): the large-n policy (GPConfig)."""
+        A fresh fit each round (hyperparameters by marginal likelihood, or fixed), or - fixed hyperparameters,
+        incremental mode - the previous round's factor extended by the rows observed since.  With
+        GPConfig.large_n_policy and n > svgp_threshold (the reference's SVGP switch, Bayesian6.py:589): the large-n
+        policy (GPConfig)."""
         n = self.train_X.shape[0]
         if n < 1:
             raise RuntimeError("fit_gp_model needs at least one observation")
         cfg = self.config
         self.y_tf = LogOutputStandardizer().fit(self.train_Y_raw)
         Ys = self.y_tf(self.train_Y_raw)
-        if n > self.svgp_threshold:
+        if cfg.large_n_policy and n > self.svgp_threshold:
             return self._fit_large_n(n, Ys)
         self._large_n_base = None
         grow = (not cfg.fit_hyperparameters and cfg.incremental_updates and self.gp_model is not None
@@ -273,6 +281,7 @@ class BayesianOptimizer:
             self.gp_model.append_observations(self.x_tf(self.train_X[n_old:]), Ys[n_old:])
             return self.gp_model
         self.gp_model = None  # the previous round's factor is released before the next one is allocated
+        self._check_device_budget(n, n)
         self.x_tf = LogInputStandardizer(self._bounds_t()).fit(self.train_X)
         self.gp_model = ExactGP(self.x_tf(self.train_X), Ys, self._kernel_params(), engine=self.engine,
                                 jitter_schedule=(0.0, cfg.jitter_val, 1e-2))
@@ -289,13 +298,39 @@ class BayesianOptimizer:
         npad = -(-int(n) // _capi.GPX_TILE) * _capi.GPX_TILE
         return 2 * npad * npad * 8 + 2 * npad * 64 * 8
 
+    def _free_device_bytes(self) -> Optional[int]:
+        """Device memory a new factor can take: the driver's free memory plus what torch's caching allocator holds
+        unused (a factor released just before is still reserved there), or None off the GPU."""
+        if not (torch.cuda.is_available() and getattr(self.gp_device, "type", "cpu") == "cuda"):
+            return None
+        torch.cuda.empty_cache()
+        free = torch.cuda.mem_get_info(self.gp_device)[0]
+        return int(free + torch.cuda.memory_reserved(self.gp_device) - torch.cuda.memory_allocated(self.gp_device))
+
+    def _check_device_budget(self, n: int, cap: int) -> int:
+        """The capacity (>= n) an exact factor can reserve within GPConfig.large_n_memory_fraction of the free device
+        memory; MemoryError naming the numbers when even n does not fit."""
+        free = self._free_device_bytes()
+        if free is None:
+            return cap
+        budget = self.config.large_n_memory_fraction * free
+        while cap > n and self.exact_gp_bytes(cap) > budget:
+            cap = max(n, int(0.9 * cap))
+        if self.exact_gp_bytes(cap) > budget:
+            raise MemoryError(f"exact GP at n={n} needs {self.exact_gp_bytes(n) / 1e9:.1f} GB of device memory, "
+                              f"{budget / 1e9:.1f} GB available (GPConfig.large_n_memory_fraction)")
+        return cap
+
     def _fit_large_n(self, n: int, Ys: torch.Tensor):
         """n > svgp_threshold: exact posterior over all n points with hyperparameters from a subsample fit, new rows
         folded in by the bordered update between rebuilds (GPConfig.large_n_refit_growth)."""
         cfg = self.config
         gp = self.gp_model
+        # rebuild when n has grown by large_n_refit_growth, or would outgrow the reserved capacity (the bordered update
+        # would otherwise grow the buffers outside the memory budget, GPEngine.append)
         rebuild = (gp is None or self._large_n_base is None or self.x_tf is None
-                   or n >= cfg.large_n_refit_growth * self._large_n_base or gp.train_X.shape[0] > n)
+                   or n >= cfg.large_n_refit_growth * self._large_n_base or gp.train_X.shape[0] > n
+                   or n > max(gp.capacity, gp.train_X.shape[0]))
         if not rebuild:
             n_old = gp.train_X.shape[0]
             if n_old < n:
@@ -306,20 +341,13 @@ class BayesianOptimizer:
         self.gp_model = gp = None  # release the previous factor (2 n^2 doubles) before the rebuild allocates
         # room for the rows still to come, within the device memory budget
         cap = n if self.target_total is None else max(n, min(int(self.target_total), int(cfg.large_n_refit_growth * n)))
-        if torch.cuda.is_available() and getattr(self.gp_device, "type", "cpu") == "cuda":
-            free = torch.cuda.mem_get_info(self.gp_device)[0]
-            budget = cfg.large_n_memory_fraction * free
-            while cap > n and self.exact_gp_bytes(cap) > budget:
-                cap = max(n, int(0.9 * cap))
-            if self.exact_gp_bytes(cap) > budget:
-                raise MemoryError(f"exact GP at n={n} needs {self.exact_gp_bytes(n) / 1e9:.1f} GB of device memory, "
-                                  f"{budget / 1e9:.1f} GB available (GPConfig.large_n_memory_fraction)")
+        cap = self._check_device_budget(n, cap)
         self.x_tf = LogInputStandardizer(self._bounds_t()).fit(self.train_X)
         Xs = self.x_tf(self.train_X)
         jit = (0.0, cfg.jitter_val, 1e-2)
         if cfg.fit_hyperparameters:
             m = int(self.svgp_threshold)
-            sub = np.sort(self._rng.choice(n, size=m, replace=False))
+            sub = np.sort(self._subsample_rng.choice(n, size=m, replace=False))
             sub_t = torch.as_tensor(sub, device=Xs.device)
             sub_gp = ExactGP(Xs[sub_t], Ys[sub_t], params, engine=self.engine, jitter_schedule=jit)
             sub_gp.fit_hyperparameters(cfg.prior_set, options=cfg.mll_options)

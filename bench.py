@@ -171,8 +171,9 @@ def cpu_baseline(X, y, Xs_np, kind, acq, ls, sample, reps=5):
 
 def other_configs(eng, dev, seed):
     """Side measurements at N=1 of the other GPU configs of BASELINE.json (not the headline `value`):
-    configs[2] n=16384 d=8 Matern-5/2 posterior update, configs[4] n=4096 d=16 fp32 covariance build + UCB sweep,
-    and the north star's n = 1024 point (update + EI sweep)."""
+    configs[2] n=16384 d=8 Matern-5/2 posterior update and a whole n = 16384 step (update + L^-T + 2^20-candidate
+    logEI sweep), configs[4] n=4096 d=16 fp32 covariance build + UCB sweep, and the north star's n = 1024 point
+    (update + EI sweep)."""
     out = {}
     X_np, y_np = synthetic.problem(16384, 8, seed + 7)
     X, y = torch.tensor(X_np, device=dev), torch.tensor(y_np, device=dev)
@@ -197,7 +198,35 @@ def other_configs(eng, dev, seed):
                                      "triangular solves)", "fit_ms": 1e3 * t, "updates_per_s": 1.0 / t,
                          "update_tflops_n3_over_3": 16384.0 ** 3 / 3 / t / 1e12,
                          "inverse_ms_for_a_following_sweep": 1e3 * ti}
-    del st, X, y
+    # the north star's n = 16k point for the acquisition rate: one whole step at configs[2]'s model, i.e. the posterior
+    # update, the L^-T its sweep needs and a 2^20-candidate logEI sweep + argmax (after one untimed step)
+    Xs16 = torch.tensor(synthetic.sobol(1 << 20, 8, seed + 8), device=dev)
+    bf16 = float(y_np.max())
+
+    def step16():
+        s16 = eng.fit(X, y, p, check=False, out=st)
+        return eng.acquire(s16, Xs16, "logei", best_f=bf16)
+
+    step16()
+    torch.cuda.synchronize()
+    eng.timing_reset()
+    eng.timing_enable(["trmm"])
+    a = time.perf_counter()
+    bv, bi = step16()
+    torch.cuda.synchronize()
+    t16 = time.perf_counter() - a
+    trmm16_ms, trmm16_n = eng.timing_query("trmm")
+    eng.timing_disable()
+    if st.pivot_failure() >= 0:
+        raise RuntimeError("n=16384 sweep: Cholesky failed")
+    chunk16 = (1 << 20) / max(trmm16_n, 1)
+    trmm16_tf = 16384.0 ** 2 * chunk16 / (trmm16_ms / max(trmm16_n, 1) * 1e-3) / 1e12
+    out["n=16384 sweep"] = {"workload": "n=16384 d=8 Matern-5/2 fp64: posterior update + L^-T + 1048576-candidate "
+                                        "logEI sweep + argmax (one step)", "ms_per_step": 1e3 * t16,
+                            "acq_cands_per_s": (1 << 20) / t16, "trmm_tflops": trmm16_tf,
+                            "trmm_frac": trmm16_tf / FP64_PEAK_TFLOPS, "trmm_launches": trmm16_n,
+                            "best_index": int(bi.item())}
+    del st, X, y, Xs16
     torch.cuda.empty_cache()
     X_np, y_np = synthetic.problem(4096, 16, seed + 11)
     Xs_np = synthetic.sobol(1 << 20, 16, seed + 12)

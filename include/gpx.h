@@ -132,9 +132,7 @@ size_t gpx_acq_params_size(void);
 
 /* Per-handle options (tuning and diagnostics; every default is the measured best).  gpx_create reads the environment
  * variable GPX_OPTIONS once ("name=value,name=value", names as below in lower case without the prefix, e.g.
- * "potrf_schedule=1,sweep_fused=0"); nothing else in the library reads the environment.
- *  GPX_OPT_POTRF_SCHEDULE  0 by size (default), 1 one launch per block column everywhere (today the same schedule;
- *                          the persistent dataflow variant, measured slower, is a probe build in tools/)
+ * "sweep_fused=0,potrf_mode=1"); nothing else in the library reads the environment.
  *  GPX_OPT_SPIN_LIMIT      polls before an in-launch hand-off (Cholesky dataflow, triangular solve) gives up and
  *                          reports GPX_INFO_TIMEOUT (default 4194304; 0 = give up at the first unmet poll: tests)
  *  GPX_OPT_SWEEP_FUSED     1 (default) the fused small-n sweep where it applies (padded n <= 256), 0 the K* + trmm path
@@ -142,13 +140,12 @@ size_t gpx_acq_params_size(void);
  *  GPX_OPT_POTRF_LAZY      multi-launch schedule: 0 by size (default), else flush the trailing update every g columns
  *  GPX_OPT_POTRF_MODE      multi-launch schedule: -1 by size (default), 0 eager panels, 1 lookahead panels */
 enum {
-  GPX_OPT_POTRF_SCHEDULE = 0,
-  GPX_OPT_SPIN_LIMIT = 1,
-  GPX_OPT_SWEEP_FUSED = 2,
-  GPX_OPT_GRAM_SPLIT = 3,
-  GPX_OPT_POTRF_LAZY = 4,
-  GPX_OPT_POTRF_MODE = 5,
-  GPX_OPT_COUNT = 6
+  GPX_OPT_SPIN_LIMIT = 0,
+  GPX_OPT_SWEEP_FUSED = 1,
+  GPX_OPT_GRAM_SPLIT = 2,
+  GPX_OPT_POTRF_LAZY = 3,
+  GPX_OPT_POTRF_MODE = 4,
+  GPX_OPT_COUNT = 5
 };
 gpx_status gpx_set_option(gpx_handle h, int32_t option, int64_t value);
 gpx_status gpx_get_option(gpx_handle h, int32_t option, int64_t* value_host);

@@ -58,6 +58,11 @@ def test_header_constants_match_python():
                       ("GPX_ACQ_EI", 0), ("GPX_ACQ_LOGEI", 1), ("GPX_ACQ_UCB", 2), ("GPX_ACQ_VARIANCE", 3),
                       ("GPX_TIMER_TRMM", 5)]:
         assert re.search(rf"\b{name} = {val}\b", hdr), name
+    # the per-handle option numbering the binding uses (the dead potrf_schedule slot was removed in round 4)
+    for name, val in _capi.OPTIONS.items():
+        assert re.search(rf"\bGPX_OPT_{name.upper()} = {val}\b", hdr), name
+    assert re.search(rf"\bGPX_OPT_COUNT = {_capi.GPX_OPT_COUNT}\b", hdr)
+    assert "POTRF_SCHEDULE" not in hdr
 
 
 def test_workspace_queries_without_gpu(lib):

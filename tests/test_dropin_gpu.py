@@ -48,14 +48,15 @@ def test_dropin_gpu_model_matches_oracle_engine(tmp_path, engine):
 
 
 def test_dropin_crosses_svgp_threshold_on_gpu(tmp_path, engine):
-    """The driver's threshold (scripts/run_optimization.py:40: 3000): below it the GP is refitted by marginal
+    """The driver's threshold (scripts/run_optimization.py:40: 3000), with the opt-in large-n policy: below it the GP is
+    refitted by marginal
     likelihood each round, above it hyperparameters come from a 3000-point subsample, the exact posterior covers every
     point, and later rounds use the bordered update; the posterior then equals a fresh fit on the same data."""
     from bayesianoptimizer_amd.models import ExactGP
     from oracle import gp_oracle as O
 
     cfg = GPConfig(candidates_pool_size=2048, acq_batch_size=20, fit_hyperparameters=True, prior_set="none",
-                   mll_options={"maxiter": 15})
+                   mll_options={"maxiter": 15}, large_n_policy=True)
     opt = BayesianOptimizer(StubSimulator(), BOUNDS, str(tmp_path), n_initial_points=2990, n_batches=3, batch_size=20,
                             svgp_threshold=3000, target_total=3050, engine=engine, gp_config=cfg, seed=1)
     opt.optimize()

@@ -1,8 +1,7 @@
 """Failure reporting of the persistent launches (the triangular solve's hand-offs) when an in-launch hand-off times
 out, the per-handle options that replaced the library's environment knobs (include/gpx.h GPX_OPT_*), the pivot of a
-failing factorisation deep in the matrix, batch invariance of the factor, and the leading-dimension limit.  (The
-persistent dataflow Cholesky these tests once compared against is a probe build in tools/gpx_potrf_dag.hip: measured
-slower than the multi-launch schedule)  Reference call sites: psd_safe_cholesky [upstream] reached from
+failing factorisation deep in the matrix (eager and lookahead panel schedules), batch invariance of the factor, and the
+leading-dimension limit.  Reference call sites: psd_safe_cholesky [upstream] reached from
 optimization/Bayesian.py:89-94, jitter retry optimization/Bayesian6.py:481-488."""
 import os
 
@@ -24,15 +23,17 @@ def test_not_pd_pivot_deep(engine):
     X, _ = O.synthetic_problem(n, 8, 5)
     kp, _ = pair("rbf", 8, noise=1e-4)
     piv = 2085
-    for schedule in (0, 1):
-        engine.set_option("potrf_schedule", schedule)
+    for mode in (0, 1):  # eager panels (the default at this size) and lookahead panels with lazy flushes
+        engine.set_option("potrf_mode", mode)
+        engine.set_option("potrf_lazy", 1 if mode == 0 else 4)
         try:
             K = engine.gram(t(X), kp)
             K[piv, piv] = -1.0
             _, info = engine.potrf(K, n)
-            assert int(info.item()) == piv + 1, schedule
+            assert int(info.item()) == piv + 1, mode
         finally:
-            engine.set_option("potrf_schedule", 0)
+            engine.set_option("potrf_mode", -1)
+            engine.set_option("potrf_lazy", 0)
 
 
 def test_fit_timeout_raises_timeout_error_not_not_pd(engine):
@@ -42,15 +43,12 @@ def test_fit_timeout_raises_timeout_error_not_not_pd(engine):
     n = 4096
     X, y = O.synthetic_problem(n, 8, 21)
     kp, _ = pair("rbf", 8, noise=1e-4)
-    for schedule in (0, 1):
-        engine.set_option("potrf_schedule", schedule)
-        engine.set_option("spin_limit", 0)
-        try:
-            with pytest.raises(GPXTimeoutError):
-                engine.fit(t(X), t(y), kp)
-        finally:
-            engine.set_option("spin_limit", 1 << 22)
-            engine.set_option("potrf_schedule", 0)
+    engine.set_option("spin_limit", 0)
+    try:
+        with pytest.raises(GPXTimeoutError):
+            engine.fit(t(X), t(y), kp)
+    finally:
+        engine.set_option("spin_limit", 1 << 22)
     st = engine.fit(t(X), t(y), kp)
     assert st.pivot_failure() == -1
 
@@ -61,7 +59,6 @@ def test_potrs_timeout_reported_in_info(engine):
     n = 4096
     X, y = O.synthetic_problem(n, 8, 22)
     kp, _ = pair("rbf", 8, noise=1e-4)
-    engine.set_option("potrf_schedule", 1)
     engine.set_option("spin_limit", 0)
     try:
         st = engine.fit(t(X), t(y), kp, check=False)
@@ -72,7 +69,6 @@ def test_potrs_timeout_reported_in_info(engine):
             st.check()
     finally:
         engine.set_option("spin_limit", 1 << 22)
-        engine.set_option("potrf_schedule", 0)
 
 
 def test_batched_timeout_names_the_problem(engine):
@@ -91,28 +87,29 @@ def test_batched_timeout_names_the_problem(engine):
 
 
 def test_options_roundtrip_and_validation(engine):
-    for name, value in (("potrf_schedule", 1), ("spin_limit", 12345), ("sweep_fused", 0), ("gram_split", 2),
+    for name, value in (("spin_limit", 12345), ("sweep_fused", 0), ("gram_split", 2),
                         ("potrf_lazy", 3), ("potrf_mode", 1)):
         old = engine.get_option(name)
         engine.set_option(name, value)
         assert engine.get_option(name) == value
         engine.set_option(name, old)
         assert engine.get_option(name) == old
-    for name, bad in (("potrf_schedule", 2), ("spin_limit", -1), ("sweep_fused", 2), ("gram_split", 3),
+    for name, bad in (("spin_limit", -1), ("sweep_fused", 2), ("gram_split", 3),
                       ("potrf_lazy", 17), ("potrf_mode", 2)):
         with pytest.raises(GPXError) as e:
             engine.set_option(name, bad)
         assert e.value.status == _capi.GPX_INVALID_ARG
     assert engine.lib.gpx_set_option(engine.handle, 99, 0) == _capi.GPX_INVALID_ARG
+    assert engine.lib.gpx_set_option(engine.handle, _capi.GPX_OPT_COUNT, 0) == _capi.GPX_INVALID_ARG
 
 
 def test_options_from_environment_at_create():
-    os.environ["GPX_OPTIONS"] = "potrf_schedule=1,sweep_fused=0,spin_limit=777,bogus=5"
+    os.environ["GPX_OPTIONS"] = "potrf_mode=1,sweep_fused=0,spin_limit=777,bogus=5,potrf_schedule=1"
     try:
         e2 = GPEngine("cuda:0")
     finally:
         del os.environ["GPX_OPTIONS"]
-    assert e2.get_option("potrf_schedule") == 1
+    assert e2.get_option("potrf_mode") == 1
     assert e2.get_option("sweep_fused") == 0
     assert e2.get_option("spin_limit") == 777
     assert e2.get_option("gram_split") == 0
@@ -125,16 +122,11 @@ def test_fit_results_identical_across_pool_sizes(engine):
     n = 4096
     X, y = O.synthetic_problem(n, 8, 40)
     kp, _ = pair("rbf", 8, noise=1e-4)
-    for schedule in (0,):
-        engine.set_option("potrf_schedule", schedule)
-        try:
-            st = engine.fit(t(X), t(y), kp)
-            L1 = st.L.cpu().numpy().copy()
-            sts = engine.fit_batched(t(np.stack([X] * 4)), t(np.stack([y] * 4)), kp)
-            for s in sts:
-                np.testing.assert_array_equal(np.tril(s.L.cpu().numpy()), np.tril(L1))
-        finally:
-            engine.set_option("potrf_schedule", 0)
+    st = engine.fit(t(X), t(y), kp)
+    L1 = st.L.cpu().numpy().copy()
+    sts = engine.fit_batched(t(np.stack([X] * 4)), t(np.stack([y] * 4)), kp)
+    for s in sts:
+        np.testing.assert_array_equal(np.tril(s.L.cpu().numpy()), np.tril(L1))
 
 
 def test_matrix_leading_dimension_limit(engine):
@@ -150,3 +142,82 @@ def test_matrix_leading_dimension_limit(engine):
     assert engine.lib.gpx_potrf_f64(engine.handle, 128, p(K), 128, p(Dinv), p(info)) == _capi.GPX_OK
     torch.cuda.synchronize()
     assert int(info.item()) != 0  # the all-zero matrix is not positive definite
+
+
+@pytest.mark.parametrize("nrhs", [1, 8])
+@pytest.mark.parametrize("batch", [1, 3])
+def test_lookahead_schedule_folded_alpha_vs_oracle(engine, nrhs, batch):
+    """The forward substitution folded into the LOOKAHEAD panel schedule (potrf_mode 1, the default for padded n > 4096)
+    at a small size: alpha of the default update against the oracle, single and batched, 1 and 8 right-hand sides
+    (only the eager schedule was compared below n = 8192)."""
+    n, d = 1000, 5
+    kp, op = pair("rbf", d, noise=1e-3, const_mean=0.1)
+    probs = [O.synthetic_problem(n, d, 60 + b) for b in range(batch)]
+    Ys = [np.stack([yb * (r + 1) - 0.2 * r for r in range(nrhs)], 1) for _, yb in probs]
+    for mode, lazy in ((1, 1), (1, 3)):
+        engine.set_option("potrf_mode", mode)
+        engine.set_option("potrf_lazy", lazy)
+        try:
+            if batch == 1:
+                sts = [engine.fit(t(probs[0][0]), t(Ys[0]), kp)]
+            else:
+                sts = engine.fit_batched(t(np.stack([Xb for Xb, _ in probs])), t(np.stack(Ys)), kp)
+        finally:
+            engine.set_option("potrf_mode", -1)
+            engine.set_option("potrf_lazy", 0)
+        for b, st in enumerate(sts):
+            a = st.alpha.cpu().numpy()
+            ar = O.fit(probs[b][0], Ys[b], op).alpha.reshape(n, nrhs)
+            assert np.abs(a[:n] - ar).max() <= 1e-8 * np.abs(ar).max(), (mode, lazy, b)
+            assert not np.any(a[n:])
+
+
+def test_standalone_potrs_timeout_leaves_state_valid(engine):
+    """A timed-out standalone solve (new targets on a fitted factor) raises GPXTimeoutError from its own info word; the
+    fitted state keeps info 0, its alpha and its posterior."""
+    n = 2048
+    X, y = O.synthetic_problem(n, 8, 24)
+    kp, _ = pair("rbf", 8, noise=1e-4)
+    st = engine.fit(t(X), t(y), kp)
+    alpha0 = st.alpha.clone()
+    engine.set_option("spin_limit", 0)
+    try:
+        with pytest.raises(GPXTimeoutError):
+            engine.potrs(st, t(y * 0.5))
+    finally:
+        engine.set_option("spin_limit", 1 << 22)
+    assert int(st.info.item()) == 0 and st.pivot_failure() == -1
+    assert torch.equal(st.alpha, alpha0)
+    a2 = engine.potrs(st, t(y * 0.5))
+    torch.testing.assert_close(a2, alpha0 * 0.5, rtol=1e-12, atol=1e-14)
+
+
+def test_fit_beside_a_long_kernel_on_another_stream(engine):
+    """the backward solve is one persistent launch whose hand-offs assume its workgroups become
+    resident.  With torch DGEMMs (~100 ms) queued on a second stream first, so that they hold CUs while the fit's
+    launches arrive, the fit must either complete with the same alpha bit for bit or raise GPXTimeoutError - never
+    return NaN or a wrong alpha silently."""
+    n = 4096
+    X, y = O.synthetic_problem(n, 8, 25)
+    kp, _ = pair("rbf", 8, noise=1e-4)
+    ref = engine.fit(t(X), t(y), kp)
+    alpha_ref = ref.alpha.clone()
+    side = torch.cuda.Stream(device=engine.device)
+    A = torch.randn(6144, 6144, dtype=torch.float64, device=engine.device) / 6144 ** 0.5
+    torch.cuda.synchronize()
+    outcomes = []
+    for _ in range(3):
+        with torch.cuda.stream(side):
+            B = A
+            for _ in range(8):
+                B = A @ B
+        try:
+            st = engine.fit(t(X), t(y), kp)
+            torch.cuda.synchronize()
+            assert torch.isfinite(st.alpha).all()
+            assert torch.equal(st.alpha, alpha_ref)
+            outcomes.append("ok")
+        except GPXTimeoutError:
+            torch.cuda.synchronize()
+            outcomes.append("timeout")
+    assert outcomes.count("ok") >= 1, outcomes

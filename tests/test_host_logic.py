@@ -234,7 +234,7 @@ def test_dropin_large_n_policy_switches_at_threshold(tmp_path):
     drop-in keeps the exact posterior over all points but fits hyperparameters on a threshold-sized subsample only and
     folds later rows in by the bordered update; below it every round refits by marginal likelihood."""
     cfg = GPConfig(candidates_pool_size=256, acq_batch_size=6, fit_hyperparameters=True, prior_set="none",
-                   mll_options={"maxiter": 8})
+                   mll_options={"maxiter": 8}, large_n_policy=True)
     eng = OracleEngine()
     opt = BayesianOptimizer(StubSimulator(), BOUNDS, str(tmp_path), n_initial_points=24, n_batches=4, batch_size=6,
                             svgp_threshold=28, target_total=48, engine=eng, gp_config=cfg, seed=5)
@@ -253,7 +253,8 @@ def test_dropin_large_n_policy_switches_at_threshold(tmp_path):
 
 
 def test_dropin_large_n_rebuilds_after_growth(tmp_path):
-    cfg = GPConfig(candidates_pool_size=128, acq_batch_size=8, fit_hyperparameters=False, large_n_refit_growth=1.5)
+    cfg = GPConfig(candidates_pool_size=128, acq_batch_size=8, fit_hyperparameters=False, large_n_refit_growth=1.5,
+                   large_n_policy=True)
     eng = OracleEngine()
     opt = BayesianOptimizer(StubSimulator(), BOUNDS, str(tmp_path), n_initial_points=20, n_batches=4, batch_size=8,
                             svgp_threshold=16, target_total=52, engine=eng, gp_config=cfg, seed=6)
@@ -263,3 +264,34 @@ def test_dropin_large_n_rebuilds_after_growth(tmp_path):
     assert opt._large_n_base == 36
     assert 20 in eng.calls["fit_n"] and 36 in eng.calls["fit_n"]
     assert opt.exact_gp_bytes(100_000) == 2 * 100_096 ** 2 * 8 + 2 * 100_096 * 64 * 8
+
+
+def test_dropin_default_refits_every_round_past_the_threshold(tmp_path):
+    """Default GPConfig (large_n_policy off): past svgp_threshold every round is still a full marginal-
+    likelihood refit on ALL points, as the reference refits its surrogate every round (Bayesian7.py:639) and keeps
+    svgp_threshold only for compatibility (Bayesian7.py:207); no subsample is drawn."""
+    cfg = GPConfig(candidates_pool_size=256, acq_batch_size=6, fit_hyperparameters=True, prior_set="none",
+                   mll_options={"maxiter": 4})
+    eng = OracleEngine()
+    opt = BayesianOptimizer(StubSimulator(), BOUNDS, str(tmp_path), n_initial_points=24, n_batches=3, batch_size=6,
+                            svgp_threshold=16, target_total=42, engine=eng, gp_config=cfg, seed=5)
+    opt.optimize()
+    assert opt._large_n_base is None
+    assert {24, 30, 36} <= eng.calls["mll_n"], eng.calls["mll_n"]
+    assert eng.calls.get("append", 0) == 0
+
+
+def test_large_n_subsample_draws_do_not_shift_candidate_draws(tmp_path):
+    """The large-n policy's subsample comes from its own RNG stream: the optimizer's candidate stream (self._rng) is the
+    same with the policy on or off."""
+    streams = []
+    for policy in (False, True):
+        cfg = GPConfig(candidates_pool_size=64, acq_batch_size=4, fit_hyperparameters=True, prior_set="none",
+                       mll_options={"maxiter": 2}, large_n_policy=policy)
+        opt = BayesianOptimizer(StubSimulator(), BOUNDS, str(tmp_path / str(policy)), n_initial_points=20,
+                                n_batches=1, batch_size=4, svgp_threshold=12, target_total=20, engine=OracleEngine(),
+                                gp_config=cfg, seed=9)
+        opt.optimize()
+        opt.fit_gp_model()  # n = 20 > 12: with the policy on, this draws a subsample
+        streams.append(opt._rng.random(4))
+    np.testing.assert_array_equal(streams[0], streams[1])
