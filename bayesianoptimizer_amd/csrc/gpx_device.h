@@ -29,6 +29,14 @@ __device__ __forceinline__ double cov_from_r2_f32(int kind, double outputscale, 
   return outputscale * (lin + (double)m);
 }
 
+// Squared distance in GPyTorch's expanded form [upstream]: ||a||^2 + ||b||^2 - 2 a.b clamped at 0.  The clamp is written
+// so that a NaN input stays NaN (fmax would turn it into 0: a NaN training input must still fail the Cholesky, and a NaN
+// candidate must still score NaN).
+__device__ __forceinline__ double sqdist_expanded(double na, double nb, double dot) {
+  const double x = fma(-2.0, dot, na + nb);
+  return x < 0.0 ? 0.0 : x;
+}
+
 // Linear index t over the lower triangle of an m x m block grid (row-major order of (i, j), j <= i)
 // -> (i, j).
 __device__ __forceinline__ void tri_decode(int t, int& i, int& j) {

@@ -105,6 +105,103 @@ __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, in
   }
 }
 
+// fp64 covariance build with the distance's cross term on the matrix cores (GPyTorch's own arithmetic [upstream]:
+// ||a||^2 + ||b||^2 - 2 a.b on centred, lengthscale-scaled inputs, clamped at 0, exactly 0 for a point with itself).
+// The difference form above spends ~2 d VALU ops and d LDS reads per element on the distance (16 + 8 at d = 8) beside
+// ~22 for exp; here a.b of a 16 x 16 block is DMAX/4 v_mfma_f64_16x16x4 and the element epilogue is r2 = max(na + nb -
+// 2 a.b, 0) and the covariance.  Centring: by the mean of the tile's (valid) row block, so a tile depends only on its
+// own rows and columns (an appended row block reproduces a refit bit for bit) and |a|, |b| stay O(spread / lengthscale);
+// the gap to the difference form is O(eps (|a|^2 + |b|^2)) per entry (bounded in tests/test_oracle.py).  The ARD linear
+// term of ScaleKernel(Linear + Matern) is a second MFMA dot (raw x_i v against raw x_j).
+// Wave w owns the 16-row strip(s) of the tile's rows and the 16-column blocks jb; the accumulator layout of
+// v_mfma_f64_16x16x4 gives each lane rows (lane >> 4) + 4 r of column lane & 15 of a block, so a store instruction writes
+// four 128-byte row segments.
+template <int DMAX, int KIND>
+__global__ void __launch_bounds__(WG) gram_mfma_kernel(gpx_kernel_params p, int n, int t0, const double* __restrict__ X,
+                                                       int64_t ldx, double* __restrict__ K, int64_t ldk, int64_t sx,
+                                                       int64_t sk, int32_t* __restrict__ info,
+                                                       unsigned long long* __restrict__ zero, int64_t zero_words) {
+  if (info && blockIdx.x == 0 && blockIdx.z == 0 && threadIdx.x == 0) info[blockIdx.y] = 0;
+  if (zero) {
+    const int64_t nwg = (int64_t)gridDim.x * gridDim.y * gridDim.z;
+    const int64_t wg = blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z);
+    for (int64_t e = wg * WG + threadIdx.x; e < zero_words; e += nwg * WG) zero[e] = 0ull;
+  }
+  X += blockIdx.y * sx;
+  K += blockIdx.y * sk;
+  constexpr bool lin = (KIND == GPX_KERNEL_SCALE_LINEAR_MATERN52);
+  constexpr int KS = DMAX / 4;  // MFMA k-steps
+  // a, b: centred scaled inputs (k >= d zero); ra: raw x_i * linear variance, rb: raw x_j; na, nb: squared norms
+  __shared__ double sa[NB][DMAX + 1], sb[NB][DMAX + 1], ra[lin ? NB : 1][DMAX + 1], rb[lin ? NB : 1][DMAX + 1];
+  __shared__ double na[NB], nb[NB], cen[DMAX];
+  int ti, tj;
+  tri_decode(t0 + (int)blockIdx.x, ti, tj);
+  const int i0 = ti * NB, j0 = tj * NB;
+  const int d = p.d, t = threadIdx.x;
+  const int nv = n - i0 < NB ? n - i0 : NB;  // valid rows of the row block (<= 0: all padding)
+  for (int e = t; e < NB * DMAX; e += WG) {
+    const int r = e / DMAX, k = e % DMAX;
+    double xi = 0.0, xj = 0.0;
+    if (k < d) {
+      if (i0 + r < n) xi = X[(int64_t)(i0 + r) * ldx + k];
+      if (j0 + r < n) xj = X[(int64_t)(j0 + r) * ldx + k];
+    }
+    sa[r][k] = (k < d) ? xi / p.lengthscale[k] : 0.0;
+    sb[r][k] = (k < d) ? xj / p.lengthscale[k] : 0.0;
+    if constexpr (lin) {
+      ra[r][k] = (k < d) ? xi * p.linear_variance[k] : 0.0;
+      rb[r][k] = xj;
+    }
+  }
+  __syncthreads();
+  if (t < DMAX) {  // centre: mean of the valid rows of the row block, summed in row order
+    double s = 0.0;
+    for (int r = 0; r < nv; ++r) s += sa[r][t];
+    cen[t] = nv > 0 ? s / nv : 0.0;
+  }
+  __syncthreads();
+  for (int e = t; e < NB * DMAX; e += WG) {
+    const int r = e / DMAX, k = e % DMAX;
+    sa[r][k] -= cen[k];
+    sb[r][k] -= cen[k];
+  }
+  __syncthreads();
+  if (t < 2 * NB) {
+    const int r = t & 63;
+    const double(*s)[DMAX + 1] = t < NB ? sa : sb;
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) v = fma(s[r][k], s[r][k], v);
+    (t < NB ? na : nb)[r] = v;
+  }
+  __syncthreads();
+  const int lane = t & 63, w = t >> 6, m = lane & 15, kq = lane >> 4;
+  const double diag_add = p.noise + p.jitter;
+  // gridDim.z row slices (small fits): the slice's 16-row strips x 4 column blocks, dealt to the waves
+  const int strips = 4 / gridDim.z, s0 = blockIdx.z * strips;
+  for (int b = w; b < strips * 4; b += 4) {
+    const int rs = 16 * (s0 + b / 4), cs = 16 * (b % 4);
+    d4 acc = {0.0, 0.0, 0.0, 0.0}, lac = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      acc = mfma16x16x4(sa[rs + m][4 * k + kq], sb[cs + m][4 * k + kq], acc);
+      if constexpr (lin) lac = mfma16x16x4(ra[rs + m][4 * k + kq], rb[cs + m][4 * k + kq], lac);
+    }
+    const int c = cs + m, gj = j0 + c;
+    const double nbc = nb[c];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = rs + kq + 4 * r, gi = i0 + rr;
+      double r2 = sqdist_expanded(na[rr], nbc, acc[r]);
+      if (gi == gj) r2 = 0.0;
+      double v = cov_from_r2(KIND, p.outputscale, r2, lin ? lac[r] : 0.0);
+      if (gi == gj) v += diag_add;
+      if (gi >= n || gj >= n) v = (gi == gj) ? 1.0 : 0.0;  // identity padding
+      K[(int64_t)gi * ldk + gj] = v;
+    }
+  }
+}
+
 hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
                        double* K, int64_t ldk, const Batch& bt, int rb0, int32_t* info, void* zero,
                        size_t zero_bytes) {
@@ -121,7 +218,7 @@ hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, 
   const int64_t zw = zero ? (int64_t)(zero_bytes / 8) : 0;
 #define GPX_GRAM_K(D, KIND)                                                                                      \
   (p.cov_fp32 ? gram_kernel<D, true, KIND><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info, zp, zw) \
-              : gram_kernel<D, false, KIND><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info, zp, zw))
+              : gram_mfma_kernel<D, KIND><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info, zp, zw))
 #define GPX_GRAM(D)                                                                                              \
   (p.kind == GPX_KERNEL_RBF        ? GPX_GRAM_K(D, GPX_KERNEL_RBF)                                               \
    : p.kind == GPX_KERNEL_MATERN52 ? GPX_GRAM_K(D, GPX_KERNEL_MATERN52)                                          \

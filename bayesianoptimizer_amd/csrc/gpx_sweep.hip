@@ -236,26 +236,65 @@ __global__ void __launch_bounds__(WG) sweep_small_kernel(gpx_kernel_params p, in
                                                          int64_t C, double* __restrict__ mu_out,
                                                          double* __restrict__ ss_out) {
   constexpr int NRB = NPAD / 16;
+  constexpr int KS = DMAX / 4;
   constexpr bool LIN = KIND == GPX_KERNEL_SCALE_LINEAR_MATERN52;
-  __shared__ double sx[NPAD][DMAX], sr[LIN ? NPAD : 1][DMAX], sa[NPAD][NR];
-  const int d = p.d;
-  for (int e = threadIdx.x; e < NPAD * DMAX; e += WG) {
+  // XT: the distance's cross term on MFMA (gram_mfma_kernel's arithmetic, centred by the mean of the training inputs):
+  // 1.745e9 / 1.784e9 vs 1.651e9 / 1.698e9 candidates/s at n = 64 / 128, but 4.60e8 vs 5.81e8 at n = 256, where the
+  // dot operands beside 16 accumulator blocks cost occupancy (tools/small_n_rates.py, profiles/r04_small_n_xterm_ab.log);
+  // npad = 256 keeps the difference form.
+  constexpr bool XT = NPAD <= 128;
+  __shared__ double sx[NPAD][DMAX + 1], sr[LIN ? NPAD : 1][DMAX + 1], sa[NPAD][NR], sn[XT ? NPAD : 1], cen[DMAX];
+  const int d = p.d, t = threadIdx.x;
+  for (int e = t; e < NPAD * DMAX; e += WG) {
     const int r = e / DMAX, k = e % DMAX;
     const double v = (k < d && r < n) ? X[(int64_t)r * ldx + k] : 0.0;
     sx[r][k] = (k < d) ? v / p.lengthscale[k] : 0.0;
-    if (LIN) sr[r][k] = (k < d) ? v * p.linear_variance[k] : 0.0;
+    if constexpr (LIN) sr[r][k] = (k < d) ? v * p.linear_variance[k] : 0.0;
   }
-  for (int e = threadIdx.x; e < NPAD * NR; e += WG) {
+  for (int e = t; e < NPAD * NR; e += WG) {
     const int r = e / NR, q = e % NR;
     sa[r][q] = (r < n && q < nrhs) ? alpha[(int64_t)r * nrhs + q] : 0.0;
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int kr = lane >> 4;
-  const int64_t c = ((int64_t)blockIdx.x * (WG / 64) + w) * 16 + (lane & 15);
+  if constexpr (XT) {
+    if (t < DMAX) {
+      double s = 0.0;
+      for (int r = 0; r < n; ++r) s += sx[r][t];
+      cen[t] = n > 0 ? s / n : 0.0;
+    }
+    __syncthreads();
+    for (int e = t; e < NPAD * DMAX; e += WG) sx[e / DMAX][e % DMAX] -= cen[e % DMAX];
+    __syncthreads();
+    for (int r = t; r < NPAD; r += WG) {
+      double v = 0.0;
+#pragma unroll
+      for (int k = 0; k < DMAX; ++k) v = fma(sx[r][k], sx[r][k], v);
+      sn[r] = v;
+    }
+    __syncthreads();
+  }
+  const int lane = t & 63, w = t >> 6;
+  const int kr = lane >> 4, m = lane & 15;
+  const int64_t c = ((int64_t)blockIdx.x * (WG / 64) + w) * 16 + m;
   const bool valid = c < m_chunk;
-  double xs[DMAX], xr[DMAX];
-  load_point<DMAX>(p, Xs + (valid ? c * ldxs : 0), valid, xs, xr);
+  // XT: this lane's B operands of the dot (candidate m, dimensions 4 s + kr) and the candidate's squared norm; else the
+  // candidate's whole point (difference form, one K* element per lane and k-step)
+  double bo[XT ? KS : 1], br[XT ? KS : 1], nb = 0.0;
+  double xs[XT ? 1 : DMAX], xr[XT ? 1 : DMAX];
+  if constexpr (XT) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k = 4 * s + kr;
+      const double v = (valid && k < d) ? Xs[c * ldxs + k] : 0.0;
+      bo[s] = (k < d) ? v / p.lengthscale[k] - cen[k] : 0.0;
+      br[s] = v;
+      nb = fma(bo[s], bo[s], nb);
+    }
+    nb += __shfl_xor(nb, 16);
+    nb += __shfl_xor(nb, 32);
+  } else {
+    load_point<DMAX>(p, Xs + (valid ? c * ldxs : 0), valid, xs, xr);
+  }
   d4 acc[NRB];
 #pragma unroll
   for (int ib = 0; ib < NRB; ++ib) acc[ib] = (d4){0.0, 0.0, 0.0, 0.0};
@@ -265,22 +304,37 @@ __global__ void __launch_bounds__(WG) sweep_small_kernel(gpx_kernel_params p, in
   const double* __restrict__ Wl = W + (int64_t)kr * ldw + (lane & 15);
 #pragma unroll
   for (int kb = 0; kb < NRB; ++kb) {
+    // XT: a.b for the 16 rows of block kb x the wave's 16 candidates; register r of the accumulator holds row
+    // 16 kb + kr + 4 r of candidate m, i.e. exactly the B operand of k-step r below
+    d4 dot = {0.0, 0.0, 0.0, 0.0}, lac = {0.0, 0.0, 0.0, 0.0};
+    if constexpr (XT) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        dot = mfma16x16x4(sx[16 * kb + m][4 * s + kr], bo[s], dot);
+        if constexpr (LIN) lac = mfma16x16x4(sr[16 * kb + m][4 * s + kr], br[s], lac);
+      }
+    }
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int k0 = 16 * kb + 4 * ks;
       const int j = k0 + kr;
-      double r2 = 0.0;
+      double kv;
+      if constexpr (XT) {
+        kv = cov_from_r2(KIND, p.outputscale, sqdist_expanded(sn[j], nb, dot[ks]), LIN ? lac[ks] : 0.0);
+      } else {
+        double r2 = 0.0;
 #pragma unroll
-      for (int k = 0; k < DMAX; ++k) {
-        const double df = sx[j][k] - xs[k];
-        r2 += df * df;
-      }
-      double lv = 0.0;
-      if (LIN) {
+        for (int k = 0; k < DMAX; ++k) {
+          const double df = sx[j][k] - xs[k];
+          r2 += df * df;
+        }
+        double lv = 0.0;
+        if constexpr (LIN) {
 #pragma unroll
-        for (int k = 0; k < DMAX; ++k) lv += sr[j][k] * xr[k];
+          for (int k = 0; k < DMAX; ++k) lv += sr[j][k] * xr[k];
+        }
+        kv = cov_from_r2(KIND, p.outputscale, r2, lv);
       }
-      double kv = cov_from_r2(KIND, p.outputscale, r2, lv);
       kv = j < n ? kv : 0.0;
 #pragma unroll
       for (int q = 0; q < NR; ++q) mu[q] += sa[j][q] * kv;

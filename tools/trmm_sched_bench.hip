@@ -10,6 +10,8 @@
 //   S4  as S2, global loads spread over substeps 0-1 (1 per 4 MFMAs)
 //   S5  peeled + iglp_opt(0)
 //   S6  peeled + iglp_opt(1)
+//   S7  one branch-free loop body (clamped next-tile loads), compiler schedule; S8 / S9 / S10: S7 + the S3 groups /
+//       iglp_opt(0) / the S2 groups
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form=1 -I../bayesianoptimizer_amd/csrc
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -102,6 +104,30 @@ __device__ __forceinline__ void schedule() {
 
 template <int S>
 struct TileS : public Base {
+  // S >= 7: one branch-free loop body over every k-tile: the next tile's loads use a clamped k (the last trip re-loads its
+  // own tile into the idle buffer), so loads, fragment reads, MFMAs and LDS writes share one scheduling region
+  __device__ __forceinline__ void run_bf(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
+                                         int64_t ldb, int kend, double* smem) {
+    this->zero();
+    double* cur = smem;
+    double* nxt = smem + 16 * (PA + PB);
+    this->load_regs(A, lda, B, ldb, 0);
+    this->store_lds(cur, cur + 16 * PA);
+    __syncthreads();
+    for (int k0 = 0; k0 < kend; k0 += 16) {
+      const int kn = k0 + 16 < kend ? k0 + 16 : k0;
+      this->load_regs(A, lda, B, ldb, kn);
+      this->compute(cur, cur + 16 * PA);
+      this->store_lds(nxt, nxt + 16 * PA);
+      if constexpr (S == 8) schedule<3>();
+      if constexpr (S == 9) schedule<5>();
+      if constexpr (S == 10) schedule<2>();
+      __syncthreads();
+      double* t = cur;
+      cur = nxt;
+      nxt = t;
+    }
+  }
   __device__ __forceinline__ void run_s(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
                                         int64_t ldb, int kend, double* smem) {
     this->zero();
@@ -139,6 +165,8 @@ __global__ void __launch_bounds__(WG) trmm_s(const double* __restrict__ W, int64
   TileS<S> tile;
   if constexpr (S == 0)
     tile.run(Ab, ldw, Bb, C, 0, (I + 1) * TT, smem);
+  else if constexpr (S >= 7)
+    tile.run_bf(Ab, ldw, Bb, C, (I + 1) * TT, smem);
   else
     tile.run_s(Ab, ldw, Bb, C, (I + 1) * TT, smem);
   double s[Base::WN];
@@ -187,8 +215,9 @@ int main() {
     CK(hipMemcpy(K, g.data(), g.size() * 8, hipMemcpyHostToDevice));
   }
   const char* names[] = {"S0 shipped", "S1 peeled", "S2 sgb spread", "S3 sgb writes 2-3", "S4 sgb loads 0-1",
-                         "S5 iglp_opt(0)", "S6 iglp_opt(1)"};
-  constexpr int NV = 7;
+                         "S5 iglp_opt(0)", "S6 iglp_opt(1)", "S7 branch-free", "S8 bf + sgb S3",
+                         "S9 bf + iglp(0)", "S10 bf + sgb S2"};
+  constexpr int NV = 11;
   auto run = [&](int v, double* out) {
     const dim3 g(ncb * nI);
     switch (v) {
@@ -198,7 +227,11 @@ int main() {
       case 3: trmm_s<3><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
       case 4: trmm_s<4><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
       case 5: trmm_s<5><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
-      default: trmm_s<6><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      case 6: trmm_s<6><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      case 7: trmm_s<7><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      case 8: trmm_s<8><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      case 9: trmm_s<9><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      default: trmm_s<10><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
     }
   };
   hipEvent_t e0, e1;
