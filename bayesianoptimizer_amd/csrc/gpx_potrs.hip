@@ -33,6 +33,9 @@
 #ifndef GPX_POTRS_STAMP
 #define GPX_POTRS_STAMP(i)
 #endif
+#ifndef GPX_POTRS_FIT_STAMP
+#define GPX_POTRS_FIT_STAMP(i)
+#endif
 
 namespace gpx {
 
@@ -321,18 +324,18 @@ __device__ __forceinline__ void fma_bwd(double (&acc)[4][NR], const TileRegs& R,
 
 }  // namespace
 
-// Single right-hand side: D_KK formed up front, one product on the chain, the block published from registers.
+// Single right-hand side, standalone solve (forward + backward): D_KK formed up front, one product on the chain, the
+// block published from registers.  A fit's backward half is potrs_bwd_fit_1.
 __device__ void potrs_items_1(int n, int npad, const double* __restrict__ L, int64_t ldl,
                               const double* __restrict__ Dinv, const double* __restrict__ Y, int64_t ldy,
                               double const_mean, double* __restrict__ alpha, gu64* gz, gu64* ga, gu32* abort_word,
-                              unsigned limit, SolveLds1& s, int& s_abort, const double* __restrict__ zin) {
+                              unsigned limit, SolveLds1& s, int& s_abort) {
   const int t = threadIdx.x, w = t >> 6;
   const int nb = npad / SB;
   const int G = gridDim.x;
   // blocks g, g + G, ... of this workgroup: forward ascending, then backward descending (see the file comment)
   const int nown = (nb - (int)blockIdx.x + G - 1) / G;
-  // zin: z from the factorisation, backward items only
-  for (int step = zin ? nown : 0; step < 2 * nown; ++step) {
+  for (int step = 0; step < 2 * nown; ++step) {
     const bool fwd = step < nown;
     const int K = (int)blockIdx.x + (fwd ? step : 2 * nown - 1 - step) * G;
     const int64_t r0 = (int64_t)K * SB;
@@ -348,11 +351,9 @@ __device__ void potrs_items_1(int n, int npad, const double* __restrict__ L, int
     };
     if (jcount > 0) load_tile(ta, 0);  // in flight while D_KK is formed
     // the first backward item is the block of the last forward item: its D_KK is still in LDS
-    if (fwd || step != nown || zin) form_block_inverse(s, Dinv, L, ldl, K);
+    if (fwd || step != nown) form_block_inverse(s, Dinv, L, ldl, K);
     if (fwd) {
       if (t < SB) s.vs[t] = (r0 + t < n) ? Y[(r0 + t) * ldy] - const_mean : 0.0;
-    } else if (zin) {
-      if (t < SB) s.vs[t] = zin[r0 + t];
     } else if (w == 0) {
       if (!sweep_block<1>(gz + r0 * 2, 1u, s.vs, abort_word, limit) && (t & 63) == 0) s_abort = 1;
     }
@@ -466,6 +467,112 @@ __device__ void potrs_items_1(int n, int npad, const double* __restrict__ L, int
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (h == 0) alpha[r0 + c] = (r0 + c < n || aborted) ? a : 0.0;
     }
+    __syncthreads();  // LDS reuse by the next item
+  }
+}
+
+// ---- the backward half of a fit (zin: z from the factorisation's folded forward substitution), one right-hand side --
+// alpha_K = D_KK^T (z_K - sum_{J>K} L_JK^T alpha_J) for K = nb-1 .. 0, the chain running through alpha_{K+1}.  Every
+// item starts at launch time (one item per workgroup up to n = 32768), so how it prepares depends on how soon the chain
+// reaches it (d = nb - 1 - K hops after its start):
+//   d < BWD_TRIPLE  no setup: D_a, D_b and L_ba staged in LDS, and after the last subtraction alpha_b = D_b^T v_b,
+//                   v_a -= L_ba^T alpha_b, alpha_a = D_a^T v_a (three 64 x 64 products): the chain starts ~5 us after the
+//                   launch instead of after the ~10 us of forming D_KK (tools/potrs_fit_probe.hip);
+//   else            the 128 x 128 inverse D_KK formed at the start (form_block_inverse): one product after the last
+//                   subtraction (potrs_items_1's backward item, with its two register tiles).
+// Measured and not kept (profiles/r04_potrs_fit_timeline.log): precomputing P = L_{K+1,K} D_KK so that the step on the
+// chain becomes alpha_K = u - P^T alpha_{K+1} (u = D_KK^T (z_K - sum_{J>K+1} ...)) - P costs ~30 us of setup, and u then
+// depends on alpha_{K+2}, so two hops took ~9 us instead of ~6.
+constexpr int BWD_TRIPLE = 3;
+
+__device__ void potrs_bwd_fit_1(int n, int npad, const double* __restrict__ L, int64_t ldl,
+                                const double* __restrict__ Dinv, double* __restrict__ alpha, gu64* ga,
+                                gu32* abort_word, unsigned limit, SolveLds1& s, int& s_abort,
+                                const double* __restrict__ zin) {
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int nb = npad / SB;
+  const int G = gridDim.x;
+  const int nown = (nb - (int)blockIdx.x + G - 1) / G;
+  double* zw = s.zw[w];
+  for (int step = 0; step < nown; ++step) {
+    const int K = (int)blockIdx.x + (nown - 1 - step) * G;  // descending
+    const int64_t r0 = (int64_t)K * SB;
+    const int jcount = nb - 1 - K;
+    const bool triple = nb - 1 - K < BWD_TRIPLE;
+    GPX_POTRS_FIT_STAMP(0);
+    TileRegs ta, tb;
+    auto load_tile = [&](TileRegs& R, int jj) { load_tile_bwd(R, L, ldl, (int64_t)(nb - 1 - jj) * SB, r0); };
+    if (jcount > 0) load_tile(ta, 0);  // in flight during the setup
+    double* Da = s.Dk;  // triple: D_a, D_b, L_ba (row length LDT) and the produced block
+    double* Db = Da + NB * LDT;
+    double* Lba = Db + NB * LDT;
+    double* os = Lba + NB * LDT;
+    if (triple) {
+      tile_to_lds(Dinv + (int64_t)(2 * K) * NB * NB, NB, Da);
+      tile_to_lds(Dinv + (int64_t)(2 * K + 1) * NB * NB, NB, Db);
+      tile_to_lds(L + (r0 + NB) * ldl + r0, ldl, Lba);
+    } else {
+      form_block_inverse(s, Dinv, L, ldl, K);
+    }
+    if (t < SB) s.vs[t] = zin[r0 + t];
+    GPX_POTRS_FIT_STAMP(1);
+    double acc[4][1] = {{0.0}, {0.0}, {0.0}, {0.0}};
+    auto consume = [&](const TileRegs& R, int jj) {
+      if (!sweep_block<1>(ga + (int64_t)(nb - 1 - jj) * SB * 2, 2u, zw, abort_word, limit) && lane == 0) s_abort = 1;
+      fma_bwd<1>(acc, R, zw);
+    };
+    for (int jj = 0; jj < jcount; jj += 2) {  // the next tile loads while the current one's block is awaited
+      const bool two = jj + 1 < jcount;
+      if (two) load_tile(tb, jj + 1);
+      consume(ta, jj);
+      if (!two) break;
+      if (jj + 2 < jcount) load_tile(ta, jj + 2);
+      consume(tb, jj + 1);
+    }
+    acc[0][0] += xor_lane<1>(acc[0][0]);
+    GPX_POTRS_FIT_STAMP(2);
+    __syncthreads();  // s.vs, the staged blocks and every wave's abort flag
+    if ((t & 1) == 0) s.vs[t >> 1] -= acc[0][0];
+    __syncthreads();
+    const bool aborted = s_abort != 0;
+    if (triple) {
+      gemv64<1, true, false>(os + NB, Db, s.vs + NB);
+      __syncthreads();
+      gemv64<1, true, true>(s.vs, Lba, os + NB);
+      __syncthreads();
+      gemv64<1, true, false>(os, Da, s.vs);
+      __syncthreads();
+      if (aborted && t < SB) os[t] = __builtin_nan("");
+      __syncthreads();
+      publish_block<1>(ga + r0 * 2, 2u, os);
+      if (t < SB) alpha[r0 + t] = (r0 + t < n || aborted) ? os[t] : 0.0;
+    } else {
+      // alpha_K = D_KK^T v: thread (c, h) sums rows 64 h .. 64 h + 63 of column c (four independent chains)
+      const int c = t >> 1, h = t & 1;
+      double a4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int i0 = 0; i0 < NB; i0 += 16) {
+        double dd[16];
+        double2 vv[8];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dd[i] = s.Dk[(NB * h + i0 + i) * LDK + c];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) vv[i] = *reinterpret_cast<const double2*>(s.vs + NB * h + i0 + 2 * i);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          a4[(2 * i) & 3] = fma(dd[2 * i], vv[i].x, a4[(2 * i) & 3]);
+          a4[(2 * i + 1) & 3] = fma(dd[2 * i + 1], vv[i].y, a4[(2 * i + 1) & 3]);
+        }
+      }
+      double a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+      a += xor_lane<1>(a);
+      if (aborted) a = __builtin_nan("");
+      const unsigned long long u = __double_as_longlong(a);
+      __hip_atomic_store(ga + (r0 + c) * 2 + h, (2ull << 32) | (h ? (u >> 32) : (u & 0xffffffffull)), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      if (h == 0) alpha[r0 + c] = (r0 + c < n || aborted) ? a : 0.0;
+    }
+    GPX_POTRS_FIT_STAMP(5);
     __syncthreads();  // LDS reuse by the next item
   }
 }
@@ -606,7 +713,10 @@ __global__ void __launch_bounds__(WG) potrs_kernel(int n, int npad, const double
   if constexpr (NR == 1) {
     __shared__ __attribute__((aligned(16))) SolveLds1 s;
     __syncthreads();
-    potrs_items_1(n, npad, L, ldl, Dinv, Y, ldy, const_mean, alpha, gz, ga, abort_word, limit, s, s_abort, zin);
+    if (zin)
+      potrs_bwd_fit_1(n, npad, L, ldl, Dinv, alpha, ga, abort_word, limit, s, s_abort, zin);
+    else
+      potrs_items_1(n, npad, L, ldl, Dinv, Y, ldy, const_mean, alpha, gz, ga, abort_word, limit, s, s_abort);
   } else {
     __shared__ __attribute__((aligned(16))) SolveLds<NR> s;
     __syncthreads();

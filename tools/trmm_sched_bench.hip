@@ -197,6 +197,78 @@ __global__ void __launch_bounds__(WG) trmm_s(const double* __restrict__ W, int64
   }
 }
 
+// S11+: no LDS at all.  Every wave loads its own MFMA fragments straight from global memory (k-major operands: lanes
+// m = 0..15 of a k-row read 16 consecutive doubles, so each load instruction covers four full 128-byte lines), PD
+// k-steps (of 4) ahead in a register ring of PD + 1 stages; no barriers, no LDS writes or reads.  The same MFMA order per
+// accumulator as the shipped tile (k ascending), so the column sums agree bit for bit.
+template <int PD>
+__global__ void __launch_bounds__(WG) trmm_direct(const double* __restrict__ W, int64_t ldw,
+                                                  const double* __restrict__ kstar, int64_t C, int nI, int ncb,
+                                                  double* __restrict__ ss_part) {
+  constexpr int NS = PD + 1;
+  const int b = blockIdx.x;
+  const int x = b & 7, l = b >> 3, per = ncb >> 3;
+  const int I = nI - 1 - l / per, cb = 8 * (l % per) + x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int m = lane & 15, kq = lane >> 4;
+  const double* Ab = W + (int64_t)I * TT + (w >> 1) * 64 + m + (int64_t)kq * ldw;
+  const double* Bb = kstar + (int64_t)cb * TT + (w & 1) * 64 + m + (int64_t)kq * C;
+  const int nsteps = (I + 1) * TT / 4;
+  d4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
+  double a[NS][4], bb[NS][4];
+  auto load = [&](int st, int s) {
+    const int64_t ka = (int64_t)(4 * s) * ldw, kb = (int64_t)(4 * s) * C;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[st][i] = Ab[ka + 16 * i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bb[st][j] = Bb[kb + 16 * j];
+  };
+#pragma unroll
+  for (int st = 0; st < PD; ++st) load(st, st);
+  for (int s0 = 0; s0 < nsteps; s0 += NS) {
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+      const int s = s0 + st;
+      const int sn = s + PD < nsteps ? s + PD : nsteps - 1;  // clamped: the tail re-loads the last step (unused)
+      load((st + PD) % NS, sn);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x4(a[st][i], bb[st][j], acc[i][j]);
+    }
+  }
+  // column sums of squares over this wave's 64 rows, then over the two row halves (as the shipped kernel)
+  __shared__ double red[TT];
+  double sv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double v = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v += acc[i][j][r] * acc[i][j][r];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    sv[j] = v;
+  }
+  if ((w >> 1) == 1 && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[(w & 1) * 64 + 16 * j + m] = sv[j];
+  }
+  __syncthreads();
+  if ((w >> 1) == 0 && lane < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = (w & 1) * 64 + 16 * j + m;
+      ss_part[(int64_t)I * C + (int64_t)cb * TT + col] = sv[j] + red[col];
+    }
+  }
+}
+
 int main() {
   const int n = 4096, C = 32768, nI = n / TT, ncb = C / TT;
   double *W, *K, *ss0, *ss1;
@@ -216,8 +288,9 @@ int main() {
   }
   const char* names[] = {"S0 shipped", "S1 peeled", "S2 sgb spread", "S3 sgb writes 2-3", "S4 sgb loads 0-1",
                          "S5 iglp_opt(0)", "S6 iglp_opt(1)", "S7 branch-free", "S8 bf + sgb S3",
-                         "S9 bf + iglp(0)", "S10 bf + sgb S2"};
-  constexpr int NV = 11;
+                         "S9 bf + iglp(0)", "S10 bf + sgb S2", "S11 direct PD=1", "S12 direct PD=3",
+                         "S13 direct PD=5"};
+  constexpr int NV = 14;
   auto run = [&](int v, double* out) {
     const dim3 g(ncb * nI);
     switch (v) {
@@ -231,7 +304,10 @@ int main() {
       case 7: trmm_s<7><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
       case 8: trmm_s<8><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
       case 9: trmm_s<9><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
-      default: trmm_s<10><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      case 10: trmm_s<10><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      case 11: trmm_direct<1><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      case 12: trmm_direct<3><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      default: trmm_direct<5><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
     }
   };
   hipEvent_t e0, e1;
