@@ -121,6 +121,8 @@ __global__ void __launch_bounds__(WG) kstar_kernel(gpx_kernel_params p, int n, c
   for (int q = 0; q < GPX_MAX_RHS; ++q) mu[q] = 0.0;
   const int jn = n - j0 < NB ? n - j0 : NB;  // real rows of this block (<= 0 for an all-padding block)
   int j = 0;
+  // four rows in flight (independent distance / exp chains; the mean accumulates in row order)
+#pragma unroll 4
   for (; j < jn; ++j) {
     double lv = 0.0;
     if (KIND == GPX_KERNEL_SCALE_LINEAR_MATERN52) {
@@ -156,6 +158,140 @@ __global__ void __launch_bounds__(WG) kstar_kernel(gpx_kernel_params p, int n, c
   }
   for (; j < NB; ++j) kstar[(int64_t)(j0 + j) * C + c] = 0.0;
   for (int q = 0; q < nrhs; ++q) mu_part[((int64_t)jb * nrhs + q) * C + c] = mu[q];
+}
+
+// fp64 K* with the distance's cross term on the matrix cores (GPyTorch's ||a||^2 + ||b||^2 - 2 a.b clamped at 0
+// [upstream]; gram_mfma_kernel's arithmetic, centred by the mean of the workgroup's valid training rows).  A workgroup
+// owns the 64 training rows of block jb x 256 candidates, wave w the candidates 64 w .. 64 w + 63 (four 16-column MFMA
+// blocks) over the four 16-row strips.  The MFMA accumulator gives a lane rows kq + 4 r of column m of a block; before the
+// stores, each group of four registers (the four column blocks of one r) is transposed across the wave's four 16-lane
+// rows by two v_permlane32_swap + two v_permlane16_swap, so every store instruction writes one K* row of 64 consecutive
+// candidates (512 bytes) like the difference-form kernel (an untransposed first version, four 128-byte row segments per
+// instruction, ran at 3.5 vs 4.7 TB/s).  Per element: one fma, a compare and the covariance, no per-dimension VALU work.
+__device__ __forceinline__ void swap_halves(double& a, double& b, bool rows32) {
+  const unsigned long long ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+  const unsigned alo = (unsigned)ua, ahi = (unsigned)(ua >> 32), blo = (unsigned)ub, bhi = (unsigned)(ub >> 32);
+  unsigned nalo, nahi, nblo, nbhi;
+  if (rows32) {
+    const auto l = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+    nalo = l[0], nblo = l[1], nahi = h[0], nbhi = h[1];
+  } else {
+    const auto l = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+    nalo = l[0], nblo = l[1], nahi = h[0], nbhi = h[1];
+  }
+  a = __longlong_as_double(((unsigned long long)nahi << 32) | nalo);
+  b = __longlong_as_double(((unsigned long long)nbhi << 32) | nblo);
+}
+// v[q] of 16-lane row g becomes the old v[g] of row q (a 4 x 4 transpose of (lane row) x (register))
+__device__ __forceinline__ void transpose_rows4(double (&v)[4]) {
+  swap_halves(v[0], v[2], true);
+  swap_halves(v[1], v[3], true);
+  swap_halves(v[0], v[1], false);
+  swap_halves(v[2], v[3], false);
+}
+
+template <int DMAX, int KIND, bool ONE_RHS>
+__global__ void __launch_bounds__(WG) kstar_mfma_kernel(gpx_kernel_params p, int n, const double* __restrict__ X,
+                                                        int64_t ldx, const double* __restrict__ alpha, int nrhs,
+                                                        const double* __restrict__ Xs, int64_t ldxs, int64_t m_chunk,
+                                                        int64_t C, double* __restrict__ kstar,
+                                                        double* __restrict__ mu_part) {
+  constexpr bool lin = (KIND == GPX_KERNEL_SCALE_LINEAR_MATERN52);
+  constexpr int KS = DMAX / 4;
+  constexpr int NRQ = ONE_RHS ? 1 : GPX_MAX_RHS;
+  __shared__ double sa[NB][DMAX + 1], sb[WG][DMAX + 1], ra[lin ? NB : 1][DMAX + 1], rb[lin ? WG : 1][DMAX + 1];
+  __shared__ double na[NB], nb[WG], cen[DMAX], sal[NB][NRQ];
+  const int jb = blockIdx.y, j0 = jb * NB, d = p.d, t = threadIdx.x;
+  const int64_t c0 = (int64_t)blockIdx.x * WG;
+  const int nv = n - j0 < NB ? n - j0 : NB;  // valid training rows of the block (<= 0: all padding)
+  for (int e = t; e < NB * DMAX; e += WG) {
+    const int r = e / DMAX, k = e % DMAX;
+    const double v = (k < d && j0 + r < n) ? X[(int64_t)(j0 + r) * ldx + k] : 0.0;
+    sa[r][k] = (k < d) ? v / p.lengthscale[k] : 0.0;
+    if constexpr (lin) ra[r][k] = (k < d) ? v * p.linear_variance[k] : 0.0;
+  }
+  for (int e = t; e < WG * DMAX; e += WG) {
+    const int r = e / DMAX, k = e % DMAX;
+    const double v = (k < d && c0 + r < m_chunk) ? Xs[(c0 + r) * ldxs + k] : 0.0;
+    sb[r][k] = (k < d) ? v / p.lengthscale[k] : 0.0;
+    if constexpr (lin) rb[r][k] = v;
+  }
+  for (int e = t; e < NB * NRQ; e += WG) {
+    const int r = e / NRQ, q = e % NRQ;
+    sal[r][q] = (q < nrhs && j0 + r < n) ? alpha[(int64_t)(j0 + r) * nrhs + q] : 0.0;
+  }
+  __syncthreads();
+  if (t < DMAX) {
+    double s = 0.0;
+    for (int r = 0; r < nv; ++r) s += sa[r][t];
+    cen[t] = nv > 0 ? s / nv : 0.0;
+  }
+  __syncthreads();
+  for (int e = t; e < NB * DMAX; e += WG) sa[e / DMAX][e % DMAX] -= cen[e % DMAX];
+  for (int e = t; e < WG * DMAX; e += WG) sb[e / DMAX][e % DMAX] -= cen[e % DMAX];
+  __syncthreads();
+  {
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < DMAX; ++k) v = fma(sb[t][k], sb[t][k], v);
+    nb[t] = v;
+    if (t < NB) {
+      double u = 0.0;
+#pragma unroll
+      for (int k = 0; k < DMAX; ++k) u = fma(sa[t][k], sa[t][k], u);
+      na[t] = u;
+    }
+  }
+  __syncthreads();
+  const int lane = t & 63, w = t >> 6, m = lane & 15, kq = lane >> 4;
+  double mu[4][NRQ];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int q = 0; q < NRQ; ++q) mu[cb][q] = 0.0;
+  double nbc[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) nbc[cb] = nb[64 * w + 16 * cb + m];
+#pragma unroll 1
+  for (int rs = 0; rs < NB; rs += 16) {
+    double kv[4][4];  // [r][cb]: row rs + kq + 4 r, candidate 64 w + 16 cb + m
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      d4 acc = {0.0, 0.0, 0.0, 0.0}, lac = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        acc = mfma16x16x4(sa[rs + m][4 * k + kq], sb[64 * w + 16 * cb + m][4 * k + kq], acc);
+        if constexpr (lin) lac = mfma16x16x4(ra[rs + m][4 * k + kq], rb[64 * w + 16 * cb + m][4 * k + kq], lac);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = rs + kq + 4 * r;
+        double v = cov_from_r2(KIND, p.outputscale, sqdist_expanded(na[j], nbc[cb], acc[r]), lin ? lac[r] : 0.0);
+        v = j < nv ? v : 0.0;
+        kv[r][cb] = v;
+#pragma unroll
+        for (int q = 0; q < NRQ; ++q) mu[cb][q] = fma(sal[j][q], v, mu[cb][q]);
+      }
+    }
+    // after the transpose, register q of 16-lane row g holds row rs + q + 4 r, candidate 64 w + 16 g + m
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      transpose_rows4(kv[r]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) kstar[(int64_t)(j0 + rs + q + 4 * r) * C + c0 + 64 * w + lane] = kv[r][q];
+    }
+  }
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int q = 0; q < NRQ; ++q) {
+      double v = mu[cb][q];
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      if (kq == 0 && q < nrhs) mu_part[((int64_t)jb * nrhs + q) * C + c0 + 64 * w + 16 * cb + m] = v;
+    }
 }
 
 // ---- 2. triangular product + column sums of squares ------------------------------------------------------
@@ -550,15 +686,26 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
   (p.kind == GPX_KERNEL_RBF        ? GPX_KSTAR_K(D, F, GPX_KERNEL_RBF)                                             \
    : p.kind == GPX_KERNEL_MATERN52 ? GPX_KSTAR_K(D, F, GPX_KERNEL_MATERN52)                                        \
                                    : GPX_KSTAR_K(D, F, GPX_KERNEL_SCALE_LINEAR_MATERN52))
-#define GPX_KSTAR(D) (p.cov_fp32 ? GPX_KSTAR_F(D, true) : GPX_KSTAR_F(D, false))
+#define GPX_KSTAR_M(D, K)                                                                                          \
+  (nrhs == 1 ? kstar_mfma_kernel<D, K, true><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk, C, \
+                                                                      b.kstar, b.mu_part)                            \
+             : kstar_mfma_kernel<D, K, false><<<g, WG, 0, c->stream>>>(p, n, X, ldx, alpha, nrhs, Xs, ldxs, m_chunk,  \
+                                                                       C, b.kstar, b.mu_part))
+#define GPX_KSTAR_MK(D)                                                                                            \
+  (p.kind == GPX_KERNEL_RBF        ? GPX_KSTAR_M(D, GPX_KERNEL_RBF)                                                \
+   : p.kind == GPX_KERNEL_MATERN52 ? GPX_KSTAR_M(D, GPX_KERNEL_MATERN52)                                           \
+                                   : GPX_KSTAR_M(D, GPX_KERNEL_SCALE_LINEAR_MATERN52))
+#define GPX_KSTAR(D) (p.cov_fp32 ? GPX_KSTAR_F(D, true) : GPX_KSTAR_MK(D))
     if (p.d <= 4)
       GPX_KSTAR(4);
     else if (p.d <= 8)
       GPX_KSTAR(8);
     else if (p.d <= 16)
       GPX_KSTAR(16);
-    else
-      GPX_KSTAR(32);
+    else  // d > 16: the difference form (the MFMA kernel's candidate tile would not fit 64 KB of LDS)
+      p.cov_fp32 ? GPX_KSTAR_F(32, true) : GPX_KSTAR_F(32, false);
+#undef GPX_KSTAR_MK
+#undef GPX_KSTAR_M
 #undef GPX_KSTAR
 #undef GPX_KSTAR_F
 #undef GPX_KSTAR_K
