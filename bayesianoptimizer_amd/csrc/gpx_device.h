@@ -37,6 +37,32 @@ __device__ __forceinline__ double sqdist_expanded(double na, double nb, double d
   return x < 0.0 ? 0.0 : x;
 }
 
+// Exchange of the 16-lane rows of two registers (rows32: rows 2, 3 of a with rows 0, 1 of b, v_permlane32_swap; else
+// the odd rows of a with the even rows of b, v_permlane16_swap), both 32-bit halves.
+__device__ __forceinline__ void swap_halves(double& a, double& b, bool rows32) {
+  const unsigned long long ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+  const unsigned alo = (unsigned)ua, ahi = (unsigned)(ua >> 32), blo = (unsigned)ub, bhi = (unsigned)(ub >> 32);
+  unsigned nalo, nahi, nblo, nbhi;
+  if (rows32) {
+    const auto l = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+    nalo = l[0], nblo = l[1], nahi = h[0], nbhi = h[1];
+  } else {
+    const auto l = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+    nalo = l[0], nblo = l[1], nahi = h[0], nbhi = h[1];
+  }
+  a = __longlong_as_double(((unsigned long long)nahi << 32) | nalo);
+  b = __longlong_as_double(((unsigned long long)nbhi << 32) | nblo);
+}
+// v[q] of 16-lane row g becomes the old v[g] of row q (a 4 x 4 transpose of (lane row) x (register))
+__device__ __forceinline__ void transpose_rows4(double (&v)[4]) {
+  swap_halves(v[0], v[2], true);
+  swap_halves(v[1], v[3], true);
+  swap_halves(v[0], v[1], false);
+  swap_halves(v[2], v[3], false);
+}
+
 // Linear index t over the lower triangle of an m x m block grid (row-major order of (i, j), j <= i)
 // -> (i, j).
 __device__ __forceinline__ void tri_decode(int t, int& i, int& j) {

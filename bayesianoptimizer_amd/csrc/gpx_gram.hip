@@ -115,7 +115,9 @@ __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, in
 // term of ScaleKernel(Linear + Matern) is a second MFMA dot (raw x_i v against raw x_j).
 // Wave w owns the 16-row strip(s) of the tile's rows and the 16-column blocks jb; the accumulator layout of
 // v_mfma_f64_16x16x4 gives each lane rows (lane >> 4) + 4 r of column lane & 15 of a block, so a store instruction writes
-// four 128-byte row segments.
+// four 128-byte row segments.  Measured and not kept (profiles/r04_gram128_ab.log, r04_gram_rowstore_ab.log): whole-row
+// 512-byte stores through a permlane transpose (as kstar_mfma_kernel does) 34.0 vs 28.9 us at n = 4096, and 128 x 128
+// tiles 33.5 vs 29.3 us (331 vs 365 us at n = 16384).
 template <int DMAX, int KIND>
 __global__ void __launch_bounds__(WG) gram_mfma_kernel(gpx_kernel_params p, int n, int t0, const double* __restrict__ X,
                                                        int64_t ldx, double* __restrict__ K, int64_t ldk, int64_t sx,

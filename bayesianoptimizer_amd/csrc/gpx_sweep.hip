@@ -168,30 +168,6 @@ __global__ void __launch_bounds__(WG) kstar_kernel(gpx_kernel_params p, int n, c
 // rows by two v_permlane32_swap + two v_permlane16_swap, so every store instruction writes one K* row of 64 consecutive
 // candidates (512 bytes) like the difference-form kernel (an untransposed first version, four 128-byte row segments per
 // instruction, ran at 3.5 vs 4.7 TB/s).  Per element: one fma, a compare and the covariance, no per-dimension VALU work.
-__device__ __forceinline__ void swap_halves(double& a, double& b, bool rows32) {
-  const unsigned long long ua = __double_as_longlong(a), ub = __double_as_longlong(b);
-  const unsigned alo = (unsigned)ua, ahi = (unsigned)(ua >> 32), blo = (unsigned)ub, bhi = (unsigned)(ub >> 32);
-  unsigned nalo, nahi, nblo, nbhi;
-  if (rows32) {
-    const auto l = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
-    const auto h = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
-    nalo = l[0], nblo = l[1], nahi = h[0], nbhi = h[1];
-  } else {
-    const auto l = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
-    const auto h = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
-    nalo = l[0], nblo = l[1], nahi = h[0], nbhi = h[1];
-  }
-  a = __longlong_as_double(((unsigned long long)nahi << 32) | nalo);
-  b = __longlong_as_double(((unsigned long long)nbhi << 32) | nblo);
-}
-// v[q] of 16-lane row g becomes the old v[g] of row q (a 4 x 4 transpose of (lane row) x (register))
-__device__ __forceinline__ void transpose_rows4(double (&v)[4]) {
-  swap_halves(v[0], v[2], true);
-  swap_halves(v[1], v[3], true);
-  swap_halves(v[0], v[1], false);
-  swap_halves(v[2], v[3], false);
-}
-
 template <int DMAX, int KIND, bool ONE_RHS>
 __global__ void __launch_bounds__(WG) kstar_mfma_kernel(gpx_kernel_params p, int n, const double* __restrict__ X,
                                                         int64_t ldx, const double* __restrict__ alpha, int nrhs,
