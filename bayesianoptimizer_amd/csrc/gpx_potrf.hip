@@ -357,7 +357,7 @@ __device__ __forceinline__ void load_tile_lds(const double* __restrict__ G, int6
 template <int NR, int SPLIT>
 __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, int c, int p, int h, int nblk, int c0,
                                            double* __restrict__ Dinv, int32_t* __restrict__ info, double* lds,
-                                           const PotrfFwd& f) {
+                                           const PotrfFwd& f, int32_t* __restrict__ done = nullptr) {
   constexpr int PROWS = NB / SPLIT;  // rows of A_ic this workgroup owns
   double* sA = lds;             // A_cc -> L_cc
   double* sP = sA + NB * LD64;  // A_ic -> L_ic (p > 0)
@@ -493,6 +493,11 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
     if (c > 0)
       for (int e = t; e < PROWS * NR; e += WG) f.r[(int64_t)row0 * NR + e] = sR[e];
   }
+  if (done) {  // decoupled trailing update: publish "PROWS more rows of column c" (write-through stores, drained)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) __hip_atomic_fetch_add(done + c, PROWS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // Trailing workgroup of a flush launch c: 128x128 tile `tile` of the lower triangle of block columns >= cfirst,
@@ -533,14 +538,9 @@ __device__ __forceinline__ void trail_tile(int t, int T, int M, int xmap, int& I
   I = J = 0;  // not reached: p < T
 }
 
-__device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t lda, int c, int nblk, int k0, int cfirst,
-                                              int tile, int ntile, int xmap, double* lds) {
-  const int m = nblk - cfirst;
-  const int M = (m + 1) / 2;
-  const int c0 = nblk - 2 * M;
-  int I, J;
-  trail_tile(tile, ntile, M, xmap, I, J);
-  const int r0 = c0 + 2 * I, q0 = c0 + 2 * J;
+// The 128x128 tile with origin at 64-block (r0, q0): A -= sum_{k = k0}^{c-1} L_{r0..,k} L_{q0..,k}^T.
+__device__ __forceinline__ void trailing_tile_at(double* __restrict__ A, int64_t lda, int c, int k0, int cfirst, int r0,
+                                                 int q0, double* lds) {
   const double* Li = A + (int64_t)r0 * NB * lda + (int64_t)k0 * NB;
   const double* Lj = A + (int64_t)q0 * NB * lda + (int64_t)k0 * NB;
   double* C = A + (int64_t)r0 * NB * lda + (int64_t)q0 * NB;
@@ -579,6 +579,14 @@ __device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t ld
   }
 }
 
+__device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t lda, int c, int nblk, int k0, int cfirst,
+                                              int tile, int ntile, int xmap, double* lds) {
+  const int M = (nblk - cfirst + 1) / 2, c0 = nblk - 2 * M;
+  int I, J;
+  trail_tile(tile, ntile, M, xmap, I, J);
+  trailing_tile_at(A, lda, c, k0, cfirst, c0 + 2 * I, c0 + 2 * J, lds);
+}
+
 // Lookahead workgroup (mode 1) of launch c: tile (c+1+idx, c+1) of the next panel's column gets every pending
 // update, A_i,c+1 -= sum_{k = a}^{c-1} L_ik L_{c+1,k}^T with a = the first column no flush has applied to it, so
 // that the panels always apply exactly one column (K = 64 on the critical path) while the bulk of the trailing
@@ -609,11 +617,15 @@ struct StepPlan {
   int npanel, nlook, ntrail, c0, look_a, cfirst, k0, flush;
   int tbase, xmap;  // first trailing workgroup (a multiple of 8 when xmap: XCD-chunked tile order), tile order
   int split;        // panel row blocks c+1.. split into 1, 2 or 4 workgroups (panel workgroup b > 0: p = 1 + (b-1) / split)
+  int near;         // > 0: decoupled trailing update, only tile columns closer than `near` block columns (ntrail of them)
+  int32_t* sync;    // decoupled trailing update: the sync words (potrf_side_kernel), else nullptr
+  unsigned limit;   // their bounded polls (Context::spin_limit)
 };
 
 // slots > 0: the co-resident workgroup slots a problem may fill (two per CU, shared by a batch); the panel row blocks are
 // split in 2 (StepPlan::split) when the panels apply exactly one column and the split launch still fits the slots.
-inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush, int xmap = 0, int slots = 0) {
+inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush, int xmap = 0, int slots = 0,
+                          int near = 0) {
   StepPlan s;
   s.npanel = nblk - c;
   s.split = 1;
@@ -634,6 +646,14 @@ inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush,
   const int M = (flush && m > 0) ? (m + 1) / 2 : 0;
   s.ntrail = M * (M + 1) / 2;
   s.xmap = xmap;
+  s.near = 0;
+  s.sync = nullptr;
+  s.limit = 0;
+  if (near > 0 && mode == 0 && flush && c - last_flush == 1) {
+    s.near = near;
+    s.ntrail = 0;
+    for (int J = 0; J < M && nblk - 2 * M + 2 * J - c < near; ++J) s.ntrail += M - J;
+  }
   const bool eager = mode == 1 || c == 0 || c - last_flush == 1;
   if (slots > 0 && eager && s.npanel > 1) {
     for (int sp = 2; sp >= 2; sp >>= 1) {  // split 4 measured slower at n = 4096 (potrf 1.48 vs 1.46 ms), equal below
@@ -648,6 +668,102 @@ inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush,
   }
   s.tbase = xmap ? (s.npanel + s.nlook + 7) & ~7 : s.npanel + s.nlook;  // padding workgroups exit at once
   return s;
+}
+
+// ---- decoupled trailing update (GPX_OPT_POTRF_DECOUPLE, eager schedule only) -------------------------------------
+// The flush of launch c covers only the NEAR 128-tile columns (origin q0 - c < D); a persistent side kernel on a
+// second stream applies every earlier column to the FAR tiles as soon as the panels have published it, so the step
+// launches on the critical path stop paying for the bulk of the trailing matrix.  Tile (r0, q0) becomes near at
+// launch cn = q0 - D + 1: the side kernel owns its columns 0 .. cn - 2 (in SIDE_CHUNK-column products), the step
+// launches cn, cn+1, ... one column each.  The chunking is fixed, so the factor is deterministic; it differs from the
+// eager schedule's (one column per product everywhere) by rounding only.
+// Sync words (zeroed on the stream before the factorisation): done[k], k < nblk = rows of column k the panel
+// workgroups of launch k have stored (complete at (nblk - 1 - k) * 64); ver[(r0/2) * (nblk/2) + q0/2] = the columns the
+// side kernel has applied to the tile.  Producers: write-through stores, s_waitcnt vmcnt(0), barrier, one relaxed
+// agent-scope atomic (cdna_hip_programming.md §6, form R1); consumers: one lane polls, acquires, then the barrier.
+constexpr int SIDE_CHUNK = 8;  // columns per side-kernel pass over a tile (K = 512)
+
+// one lane: bounded poll until *w >= v; false on timeout or when the factorisation was aborted (info != 0)
+__device__ __forceinline__ bool poll_at_least(int32_t* w, int32_t v, int32_t* info, unsigned limit) {
+  for (unsigned spins = 0;; ++spins) {
+    if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= v) break;
+    if (spins >= limit ||
+        ((spins & 63) == 63 && __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0))
+      return false;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  (void)__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+// Near trailing workgroup `p` of launch c (tile columns in order, rows within a column): a tile that becomes near at
+// this launch first waits for the side kernel's columns.
+__device__ __forceinline__ void near_role(double* __restrict__ A, int64_t lda, int c, int nblk, const StepPlan& s, int p,
+                                          int32_t* __restrict__ info, double* lds) {
+  __shared__ int s_ok;
+  const int M = (nblk - s.cfirst + 1) / 2, c0 = nblk - 2 * M;
+  int J = 0;
+  while (p >= M - J) {
+    p -= M - J;
+    ++J;
+  }
+  const int r0 = c0 + 2 * (J + p), q0 = c0 + 2 * J, cn = q0 - s.near + 1;
+  if (c == cn && cn >= 2) {
+    if (threadIdx.x == 0) {
+      s_ok = poll_at_least(s.sync + nblk + (r0 >> 1) * (nblk >> 1) + (q0 >> 1), cn - 1, info, s.limit);
+      if (!s_ok) atomicCAS(info, 0, (int32_t)GPX_INFO_TIMEOUT);
+    }
+    __syncthreads();
+    if (!s_ok) return;
+  }
+  trailing_tile_at(A, lda, c, s.k0, s.cfirst, r0, q0, lds);
+}
+
+// The far tiles (q0 >= D + 1, in q0 order, dealt round-robin to the workgroups; one workgroup per CU): pass after pass,
+// the next SIDE_CHUNK columns of every owned tile, each once the panels have published its last column.
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
+potrf_side_kernel(double* __restrict__ A, int64_t lda, int nblk, int D, int32_t* __restrict__ sync,
+                  int32_t* __restrict__ info, unsigned limit) {
+  __shared__ __attribute__((aligned(16))) double lds[Tile128::LDS_DOUBLES];
+  __shared__ int s_ok;
+  const int qmin = (D + 2) & ~1;  // the smallest even q0 >= D + 1
+  int ntile = 0;
+  for (int q0 = qmin; q0 < nblk; q0 += 2) ntile += (nblk - q0) >> 1;
+#pragma unroll 1
+  for (int kb = 0;; kb += SIDE_CHUNK) {
+    bool any = false;
+#pragma unroll 1
+    for (int tix = blockIdx.x; tix < ntile; tix += gridDim.x) {
+      int q0 = qmin, rem = tix;
+      while (rem >= (nblk - q0) >> 1) {
+        rem -= (nblk - q0) >> 1;
+        q0 += 2;
+      }
+      const int r0 = q0 + 2 * rem, kend = q0 - D;  // this kernel's columns: 0 .. kend - 1
+      if (kb >= kend) continue;
+      any = true;
+      const int ke = min(kb + SIDE_CHUNK, kend);
+      if (threadIdx.x == 0) {
+        s_ok = poll_at_least(sync + ke - 1, (nblk - ke) * NB, info, limit);
+        if (!s_ok) atomicCAS(info, 0, (int32_t)GPX_INFO_TIMEOUT);
+      }
+      __syncthreads();
+      if (!s_ok) return;
+      // (A and lda opaque per tile: the tile's address arithmetic is not hoisted out of these loops, whose live-through
+      // values the 128x128 accumulators leave no registers for; what still spills is saved once per kernel and
+      // reloaded once per tile, one reload per k-tile of 64 MFMAs)
+      double* At = A;
+      int64_t ldt = lda;
+      asm volatile("" : "+s"(At), "+s"(ldt));
+      trailing_tile_at(At, ldt, ke, kb, 0, r0, q0, lds);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0)
+        __hip_atomic_store(sync + nblk + (r0 >> 1) * (nblk >> 1) + (q0 >> 1), ke, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!any) return;
+  }
 }
 
 // NR: 0 = no forward fold, else its right-hand-side row length (one instantiation each: the fold's registers stay out
@@ -672,11 +788,13 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, StepPlan
       f.z += blockIdx.y * f.sb;
     }
     if (s.split == 2 && b > 0)
-      panel_role<NR, 2>(A, lda, c, 1 + ((b - 1) >> 1), (b - 1) & 1, nblk, s.c0, Dinv, info, lds, f);
+      panel_role<NR, 2>(A, lda, c, 1 + ((b - 1) >> 1), (b - 1) & 1, nblk, s.c0, Dinv, info, lds, f, s.sync);
     else
-      panel_role<NR, 1>(A, lda, c, b, 0, nblk, s.c0, Dinv, info, lds, f);
+      panel_role<NR, 1>(A, lda, c, b, 0, nblk, s.c0, Dinv, info, lds, f, s.sync);
   } else if (role == 1)
     lookahead_role(A, lda, c, s.look_a, b - s.npanel, lds);
+  else if (s.near > 0)
+    near_role(A, lda, c, nblk, s, b - s.tbase, info, lds);
   else
     trailing_role(A, lda, c, nblk, s.k0, s.cfirst, b - s.tbase, s.ntrail, s.xmap, lds);
   GPX_STEP_STAMP(role, c, b, 1);
@@ -740,14 +858,21 @@ static int potrf_mode(const Context* ctx, int nblk) {
   return nblk > 64 ? 1 : 0;
 }
 
+// Near distance D of the decoupled trailing update (0 = off): eager schedule (mode 0, g = 1), one problem.  Off by
+// size until measured faster (GPX_OPT_POTRF_DECOUPLE turns it on).
+static int potrf_decouple(const Context* ctx, int nblk, int mode, int batch) {
+  if (batch != 1 || mode != 0 || potrf_lazy(ctx, nblk) != 1 || ctx->potrf_decouple <= 0) return 0;
+  return ctx->potrf_decouple < nblk ? ctx->potrf_decouple : 0;  // D >= nblk: every tile is near
+}
+
 // The plan of every launch c < cend (flush launches: c >= 1 and at least one interval after the previous flush).
 template <typename F>
-static void for_each_step(const Context* ctx, int nblk, int mode, int cend, int slots, F&& f) {
+static void for_each_step(const Context* ctx, int nblk, int mode, int cend, int slots, F&& f, int near = 0) {
   const int g = potrf_lazy(ctx, nblk);
   int last = 0;
   for (int c = 0; c < cend; ++c) {
     const bool flush = c >= 1 && c - last >= g;
-    f(c, step_plan(c, nblk, mode, last, flush, 1, slots));
+    f(c, step_plan(c, nblk, mode, last, flush, 1, slots, near));
     if (flush) last = c;
   }
 }
@@ -764,11 +889,52 @@ static int potrf_slots(Context* ctx, int batch) {
   return 2 * ctx->cu_count / (batch > 0 ? batch : 1);
 }
 
-static void launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
-                         int cbeg, int cend, const PotrfFwd& f = PotrfFwd()) {
+// The decoupled update's side stream, events and sync words (created on first use, kept by the handle).
+static hipError_t side_resources(Context* ctx, size_t bytes) {
+  hipError_t e = hipSuccess;
+  if (!ctx->side_stream) e = hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking);
+  if (e == hipSuccess && !ctx->ev_fork) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
+  if (e == hipSuccess && !ctx->ev_join) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
+  if (e == hipSuccess && ctx->sync_bytes < bytes) {
+    if (ctx->sync_buf) {
+      e = hipStreamSynchronize(ctx->stream);  // an earlier factorisation may still use the old words
+      if (e == hipSuccess) e = hipFree(ctx->sync_buf);
+      ctx->sync_buf = nullptr;
+      ctx->sync_bytes = 0;
+    }
+    if (e == hipSuccess) e = hipMalloc(&ctx->sync_buf, bytes);
+    if (e == hipSuccess) ctx->sync_bytes = bytes;
+  }
+  return e;
+}
+
+static hipError_t launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info,
+                               const Batch& bt, int cbeg, int cend, const PotrfFwd& f = PotrfFwd()) {
   const int mode = potrf_mode(ctx, nblk);
-  for_each_step(ctx, nblk, mode, cend, potrf_slots(ctx, bt.count), [&](int c, const StepPlan& s) {
+  int slots = potrf_slots(ctx, bt.count);
+  const int D = slots > 0 && cbeg == 0 && cend == nblk ? potrf_decouple(ctx, nblk, mode, bt.count) : 0;
+  int32_t* sync = nullptr;
+  if (D > 0) {
+    const size_t bytes = (size_t)(nblk + (nblk / 2) * (nblk / 2)) * sizeof(int32_t);
+    hipError_t e = side_resources(ctx, bytes);
+    if (e == hipSuccess) e = hipMemsetAsync(ctx->sync_buf, 0, bytes, ctx->stream);
+    if (e == hipSuccess) e = hipEventRecord(ctx->ev_fork, ctx->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->side_stream, ctx->ev_fork, 0);
+    if (e != hipSuccess) return e;
+    sync = ctx->sync_buf;
+    int ntile = 0;
+    for (int q0 = (D + 2) & ~1; q0 < nblk; q0 += 2) ntile += (nblk - q0) / 2;
+    const int grid = ntile < slots / 2 ? ntile : slots / 2;  // one workgroup per CU
+    if (grid > 0)
+      potrf_side_kernel<<<grid, WG, 0, ctx->side_stream>>>(A, lda, nblk, D, sync, info, ctx->spin_limit);
+    e = hipEventRecord(ctx->ev_join, ctx->side_stream);
+    if (e != hipSuccess) return e;
+    slots /= 2;  // the other slot of every CU is the step launches'
+  }
+  for_each_step(ctx, nblk, mode, cend, slots, [&](int c, StepPlan s) {
     if (c < cbeg) return;
+    s.sync = sync;
+    s.limit = ctx->spin_limit;
     const dim3 grid(s.tbase + s.ntrail, bt.count);
     if (!f.r)
       potrf_step_kernel<0><<<grid, WG, 0, ctx->stream>>>(A, lda, c, nblk, s, Dinv, info, 0, bt.k, bt.dinv, f);
@@ -776,7 +942,8 @@ static void launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double*
       potrf_step_kernel<1><<<grid, WG, 0, ctx->stream>>>(A, lda, c, nblk, s, Dinv, info, 0, bt.k, bt.dinv, f);
     else
       potrf_step_kernel<GPX_MAX_RHS><<<grid, WG, 0, ctx->stream>>>(A, lda, c, nblk, s, Dinv, info, 0, bt.k, bt.dinv, f);
-  });
+  }, D);
+  return D > 0 ? hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0) : hipSuccess;
 }
 
 static void launch_dinv(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
@@ -806,7 +973,8 @@ hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* 
     f.n = fr->n;
     f.mean = fr->mean;
   }
-  launch_steps(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, f);
+  const hipError_t es = launch_steps(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, f);
+  if (es != hipSuccess) return es;
   launch_dinv(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, W, ldw);
   const hipError_t e = hipGetLastError();
   if (e == hipSuccess && z_done && f.r) *z_done = true;

@@ -162,6 +162,72 @@ __device__ __forceinline__ int chol16_mfma(double* sA, double* sD, int o, double
 }
 
 }  // namespace gpx
+// ---- cost split of the rank-1 pivot chain (timing only: V = 2 drops X = L^{-1} and the L column capture, V = 3 drops
+// only the capture, V = 4 drops only X; results are not valid for V >= 2) ----
+#define GPX_FMAC_REST3(J)                                                                                        \
+  case J:                                                                                                        \
+    asm volatile("v_fmac_f64_dpp %0, %0, %3 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                 \
+                 "v_fmac_f64_dpp %1, %1, %3 row_newbcast:" #J " row_mask:0xf bank_mask:0xf\n\t"                 \
+                 "v_fmac_f64_dpp %2, %2, %3 row_newbcast:" #J " row_mask:0xf bank_mask:0xf"                       \
+                 : "+v"(a1), "+v"(a2), "+v"(a3)                                                                  \
+                 : "v"(ca));                                                                                     \
+    break;
+template <int J>
+__device__ __forceinline__ void fmac_rest3(double& a1, double& a2, double& a3, double ca) {
+  switch (J) {
+    GPX_FMAC_REST3(0) GPX_FMAC_REST3(1) GPX_FMAC_REST3(2) GPX_FMAC_REST3(3) GPX_FMAC_REST3(4) GPX_FMAC_REST3(5)
+    GPX_FMAC_REST3(6) GPX_FMAC_REST3(7) GPX_FMAC_REST3(8) GPX_FMAC_REST3(9) GPX_FMAC_REST3(10) GPX_FMAC_REST3(11)
+    GPX_FMAC_REST3(12) GPX_FMAC_REST3(13) GPX_FMAC_REST3(14) GPX_FMAC_REST3(15)
+  }
+}
+template <int V, int J>
+__device__ __forceinline__ void pivot_var(Blk16& b, int r, int g, int& fail, double& piv, double& arj) {
+  constexpr int GJ = J >> 2, QJ = J & 3;
+  if (!(piv > 0.0) && fail < 0) fail = J;
+  const double isq = pivot_rsq(piv);
+  const double rinv = isq * isq;
+  const double coef = (r > J) ? -arj * rinv : 0.0;
+  if (V == 4 && g == GJ) b.l[QJ] = (r >= J) ? b.a[QJ] * isq : 0.0;
+  if constexpr (J < 15) {
+    constexpr int JN = J + 1, GN = JN >> 2, QN = JN & 3;
+    fmac_pipe_first<J>(b.a[QN], coef);
+    piv = readlane_f64(b.a[QN], JN + 16 * GN);
+    arj = xrow_bcast_f64<GN>(b.a[QN]);
+    if constexpr (V == 3) {
+      const double coefx = (r == J) ? isq - 1.0 : coef;
+      fmac_pipe_rest<J>(b.a[(QN + 1) & 3], b.a[(QN + 2) & 3], b.a[(QN + 3) & 3], b.x, coef, coefx);
+    } else {
+      fmac_rest3<J>(b.a[(QN + 1) & 3], b.a[(QN + 2) & 3], b.a[(QN + 3) & 3], coef);
+    }
+  }
+}
+template <int V, int... J>
+__device__ __forceinline__ void pivots_var(Blk16& b, int r, int g, int& fail, std::integer_sequence<int, J...>) {
+  double piv = readlane_f64(b.a[0], 0), arj = xrow_bcast_f64<0>(b.a[0]);
+  (pivot_var<V, J>(b, r, g, fail, piv, arj), ...);
+}
+template <int V, int LDD>
+__device__ __forceinline__ int chol16_var(double* sA, double* sD, int o) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  Blk16 b;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    b.a[q] = sA[(o + r) * LD64 + o + 4 * g + q];
+    b.x[q] = (r == 4 * g + q) ? 1.0 : 0.0;
+    b.l[q] = 0.0;
+  }
+  int fail = -1;
+  pivots_var<V>(b, r, g, fail, std::make_integer_sequence<int, 16>{});
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = 4 * g + q;
+    sA[(o + r) * LD64 + o + c] = V == 4 ? b.l[q] : b.a[q];
+    sD[r * LDD + c] = b.x[q];
+  }
+  return fail;
+}
+
 #ifndef VARIANT
 #define VARIANT ""
 #endif
@@ -179,8 +245,10 @@ __global__ void probe(const double* A, double* L, double* D, long long* cyc) {
     const long long c0 = __builtin_readcyclecounter();
     if (V == 0)
       f = chol16<LDD>(sA, sD, 0);
-    else
+    else if (V == 1)
       f = chol16_mfma<LDD>(sA, sD, 0, sF);
+    else
+      f = chol16_var<V, LDD>(sA, sD, 0);
     __syncthreads();
     total += __builtin_readcyclecounter() - c0;
   }
@@ -228,6 +296,18 @@ int main() {
       res = fmax(res, fabs(s - hA[i * 16 + j]));
     }
   printf("chol16 (rank-1" VARIANT "): %lld cycles/call, fail=%lld\n", hc[0][0], hc[0][1]);
+  {
+    long long hv[2];
+    probe<2><<<1, 64>>>(A, L + 256, D + 256, cyc);
+    CK(hipMemcpy(hv, cyc, 16, hipMemcpyDeviceToHost));
+    printf("chol16 A-chain only (no X, no L capture): %lld cycles/call\n", hv[0]);
+    probe<3><<<1, 64>>>(A, L + 256, D + 256, cyc);
+    CK(hipMemcpy(hv, cyc, 16, hipMemcpyDeviceToHost));
+    printf("chol16 without the L capture:            %lld cycles/call\n", hv[0]);
+    probe<4><<<1, 64>>>(A, L + 256, D + 256, cyc);
+    CK(hipMemcpy(hv, cyc, 16, hipMemcpyDeviceToHost));
+    printf("chol16 without X:                        %lld cycles/call\n", hv[0]);
+  }
   printf("chol16_mfma:     %lld cycles/call, fail=%lld\n", hc[1][0], hc[1][1]);
   printf("max|dL|=%.2e max|dD|=%.2e  mfma |LL^T-A|=%.2e\n", dl, dd, res);
   printf("CHOL16 PROBE DONE\n");
