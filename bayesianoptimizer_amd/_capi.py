@@ -27,7 +27,7 @@ STATUS_NAMES = {0: "OK", 1: "NOT_PD", 2: "INVALID_ARG", 3: "HIP_ERROR", 4: "RCCL
 GPX_INFO_TIMEOUT = -(2 ** 31)  # device info word of a factorisation / solve whose in-launch hand-off timed out
 
 # per-handle options (include/gpx.h GPX_OPT_*)
-OPTIONS = {"spin_limit": 0, "sweep_fused": 1, "gram_split": 2, "potrf_lazy": 3, "potrf_mode": 4, "potrf_decouple": 5}
+OPTIONS = {"spin_limit": 0, "sweep_fused": 1, "gram_split": 2, "potrf_lazy": 3, "potrf_mode": 4}
 GPX_OPT_COUNT = len(OPTIONS)
 
 KERNEL_RBF, KERNEL_MATERN52, KERNEL_SCALE_LINEAR_MATERN52 = 0, 1, 2

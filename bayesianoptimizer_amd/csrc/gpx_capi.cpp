@@ -158,13 +158,6 @@ gpx_status gpx_destroy(gpx_handle h) {
     (void)hipEventDestroy(pt.stop);
   }
   for (auto ev : c->free_events) (void)hipEventDestroy(ev);
-  if (c->side_stream) {
-    (void)hipStreamSynchronize(c->side_stream);
-    (void)hipStreamDestroy(c->side_stream);
-  }
-  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
-  if (c->sync_buf) (void)hipFree(c->sync_buf);
   delete c;
   return GPX_OK;
 }
@@ -198,18 +191,13 @@ static gpx_status set_option(Context* c, int32_t option, int64_t v) {
       if (v < -1 || v > 1) return fail(c, GPX_INVALID_ARG, "potrf_mode must be -1, 0 or 1");
       c->potrf_mode = (int)v;
       return GPX_OK;
-    case GPX_OPT_POTRF_DECOUPLE:
-      if (v < -1 || v == 1 || v > 1024) return fail(c, GPX_INVALID_ARG, "potrf_decouple must be -1, 0 or in [2, 1024]");
-      c->potrf_decouple = (int)v;
-      return GPX_OK;
     default:
       return fail(c, GPX_INVALID_ARG, "unknown option " + std::to_string(option));
   }
 }
 
 static int option_by_name(const std::string& name) {
-  static const char* names[GPX_OPT_COUNT] = {"spin_limit", "sweep_fused", "gram_split", "potrf_lazy", "potrf_mode",
-                                                "potrf_decouple"};
+  static const char* names[GPX_OPT_COUNT] = {"spin_limit", "sweep_fused", "gram_split", "potrf_lazy", "potrf_mode"};
   for (int i = 0; i < GPX_OPT_COUNT; ++i)
     if (name == names[i]) return i;
   return -1;
@@ -251,7 +239,6 @@ gpx_status gpx_get_option(gpx_handle h, int32_t option, int64_t* value_host) {
     case GPX_OPT_GRAM_SPLIT: *value_host = c->gram_split; return GPX_OK;
     case GPX_OPT_POTRF_LAZY: *value_host = c->potrf_lazy; return GPX_OK;
     case GPX_OPT_POTRF_MODE: *value_host = c->potrf_mode; return GPX_OK;
-    case GPX_OPT_POTRF_DECOUPLE: *value_host = c->potrf_decouple; return GPX_OK;
     default: return fail(c, GPX_INVALID_ARG, "unknown option " + std::to_string(option));
   }
 }

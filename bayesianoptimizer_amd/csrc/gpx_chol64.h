@@ -176,28 +176,46 @@ __device__ __forceinline__ void chol16_pivots(Blk16& b, int r, int g, int& fail,
   (chol16_pivot_pipe<J>(b, r, g, fail, piv, arj), ...);
 }
 
-// Factor + invert the 16x16 SPD block at (o, o) of the LDS tile sA (both triangles present, symmetric) with one
-// wave: L (strict upper zeroed) back into sA, D = L^{-1} (lower, strict upper 0) into a 16x16 tile sD of row length
-// LDD.  Returns the 0-based failing pivot inside the block, or -1 (uniform).
-template <int LDD>
-__device__ __forceinline__ int chol16(double* sA, double* sD, int o) {
+// Factor + invert a 16x16 SPD block held in registers (lane = r + 16 g: b.a[q] = A[r][4g + q]): L into b.l, L^{-1}
+// into b.x.  Returns the 0-based failing pivot inside the block, or -1 (uniform).
+__device__ __forceinline__ int chol16_regs(Blk16& b) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
-  Blk16 b;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    b.a[q] = sA[(o + r) * LD64 + o + 4 * g + q];
     b.x[q] = (r == 4 * g + q) ? 1.0 : 0.0;
     b.l[q] = 0.0;
   }
   int fail = -1;
   chol16_pivots(b, r, g, fail, std::make_integer_sequence<int, 16>{});
+  return fail;
+}
+
+// L (strict upper zeroed) into the LDS tile sA at (o, o), D = L^{-1} (lower, strict upper 0) into the 16x16 tile sD of
+// row length LDD.
+template <int LDD>
+__device__ __forceinline__ void chol16_store(const Blk16& b, double* sA, double* sD, int o) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int c = 4 * g + q;
     sA[(o + r) * LD64 + o + c] = b.l[q];
     sD[r * LDD + c] = (c <= r) ? b.x[q] : 0.0;
   }
+}
+
+// Factor + invert the 16x16 SPD block at (o, o) of the LDS tile sA (both triangles present, symmetric) with one
+// wave: L back into sA, D = L^{-1} into sD (chol16_store).  Returns the failing pivot inside the block, or -1.
+template <int LDD>
+__device__ __forceinline__ int chol16(double* sA, double* sD, int o) {
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 15, g = lane >> 4;
+  Blk16 b;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) b.a[q] = sA[(o + r) * LD64 + o + 4 * g + q];
+  const int fail = chol16_regs(b);
+  chol16_store<LDD>(b, sA, sD, o);
   return fail;
 }
 

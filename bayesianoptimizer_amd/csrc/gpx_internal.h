@@ -38,13 +38,6 @@ struct Context {
   int gram_split = 0;      // 0 by size, else workgroups per Gram tile
   int potrf_lazy = 0;      // multi-launch flush interval, 0 by size
   int potrf_mode = -1;     // multi-launch panel mode, -1 by size
-  int potrf_decouple = -1; // near distance of the decoupled trailing update, 0 off, -1 by size
-  // decoupled trailing update (gpx_potrf.hip): the concurrent kernel's stream, fork / join events and the device sync
-  // words (per column: rows published; per 128-tile: columns applied), created on first use
-  hipStream_t side_stream = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  int32_t* sync_buf = nullptr;
-  size_t sync_bytes = 0;
 };
 
 // Scoped device switch of one C ABI call: makes the handle's device current and restores the caller's current device

@@ -185,34 +185,68 @@ __device__ __forceinline__ void wave_matvec16(const double* M, int ldm, const do
 // the compiler from moving the reads up)
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// SPLIT (p > 0 only; 1, 2 or 4): the workgroup owns 64 / SPLIT rows of A_ic (its row blocks RB = 0 .. 4 / SPLIT - 1);
-// SPLIT waves share a row block, wave W updating A_ic blocks (W / SPLIT, (W % SPLIT) NIC + jj), jj < NIC = 4 / SPLIT,
-// beside its A_cc blocks: at most 7 / 5 / 4 blocks per wave for SPLIT = 1 / 2 / 4.
-template <int W, bool PANEL, int NR, int SPLIT>
+// Block lists per wave (OV = 0 / 1, variant V = 0 the p = 0 workgroup, 1 a panel workgroup with 64 rows of A_ic, 2 with
+// 32 (SPLIT = 2)): kPreCC the wave's A_cc blocks (kLowerBlk indices, -1 ends), kPreIC its A_ic blocks {first, count}
+// of the block index 4 rb + j (row block rb of the workgroup's rows, column block j), kFoldRB the right-hand-side row
+// block it folds (-1: none; A_ic row blocks for p > 0, row block W of L_c for p = 0).
+//  OV = 0, even split: wave W owns the A_cc blocks W, W + 4, W + 8 and a quarter of A_ic (at most 7 / 5 blocks).
+//  OV = 1, overlapped: wave 0 updates only the first pivot block A_cc(0, 0) and factors it at once (chol16 in
+//    registers) while waves 1-3 update the other nine A_cc blocks and A_ic (3/3/3, 9/8/8, 6/6/5 blocks), so the first
+//    F step runs under the other waves' MFMAs instead of after them; wave 0 takes a fold row block in variant 1 so that
+//    no wave holds two.  Wave 0 computes its block in chol16's register layout directly: lane (r, g) needs
+//    A'[r][4g + q]; the MFMA leaves C[g + 4q][r] in that lane, so its A operand reads L_c's rows in the order
+//    perm(m) = 4 (m % 4) + m / 4 (C[g + 4q][r] = A'[4g + q][r] = A'[r][4g + q], A' symmetric) and its seed is loaded
+//    in the same order.
+constexpr int kPreCC[2][3][4][5] = {
+    {{{0, 4, 8, -1, -1}, {1, 5, 9, -1, -1}, {2, 6, -1, -1, -1}, {3, 7, -1, -1, -1}},
+     {{0, 4, 8, -1, -1}, {1, 5, 9, -1, -1}, {2, 6, -1, -1, -1}, {3, 7, -1, -1, -1}},
+     {{0, 4, 8, -1, -1}, {1, 5, 9, -1, -1}, {2, 6, -1, -1, -1}, {3, 7, -1, -1, -1}}},
+    {{{0, -1, -1, -1, -1}, {1, 2, 3, -1, -1}, {4, 5, 6, -1, -1}, {7, 8, 9, -1, -1}},
+     {{0, -1, -1, -1, -1}, {1, -1, -1, -1, -1}, {2, 3, 4, 5, -1}, {6, 7, 8, 9, -1}},
+     {{0, -1, -1, -1, -1}, {1, 2, -1, -1, -1}, {3, 4, -1, -1, -1}, {5, 6, 7, 8, 9}}}};
+constexpr int kPreIC[2][3][4][2] = {{{{0, 0}, {0, 0}, {0, 0}, {0, 0}},
+                                     {{0, 4}, {4, 4}, {8, 4}, {12, 4}},
+                                     {{0, 2}, {2, 2}, {4, 2}, {6, 2}}},
+                                    {{{0, 0}, {0, 0}, {0, 0}, {0, 0}},
+                                     {{0, 0}, {0, 8}, {8, 4}, {12, 4}},
+                                     {{0, 0}, {0, 4}, {4, 4}, {0, 0}}}};
+constexpr int kFoldRB[2][3][4] = {{{0, 1, 2, 3}, {0, 1, 2, 3}, {0, -1, 1, -1}},
+                                  {{0, 1, 2, 3}, {1, 0, 2, 3}, {-1, 0, 1, -1}}};
+constexpr int pre_count(const int* l, int n) {
+  int k = 0;
+  while (k < n && l[k] >= 0) ++k;
+  return k;
+}
+
+template <int W, bool OV, bool PANEL, int NR, int SPLIT>
 __device__ __forceinline__ void update_eager_wave(const double* __restrict__ Acc, const double* __restrict__ Aic,
                                                   const double* __restrict__ Lc, const double* __restrict__ Li,
-                                                  int64_t lda, double* sA, double* sP, int c, int rowblk0,
-                                                  const PotrfFwd& f, double* sZ, double* sR) {
-  constexpr int NCC = W < 2 ? 3 : 2;
-  constexpr int NIC = 4 / SPLIT;                 // A_ic blocks of this wave
-  constexpr int RB = W / SPLIT;                  // its A_ic row block (within the workgroup's rows)
-  constexpr int JB0 = (W % SPLIT) * NIC;         // its first A_ic column block
-  constexpr int NRI = 8 / SPLIT;                 // double2 loads of L_i per thread (64 / SPLIT rows)
-  constexpr bool FOLD_ROWS = !PANEL || (W % SPLIT) == 0;  // waves that fold their row block's right-hand side
+                                                  int64_t lda, double* sA, double* sP, double* sD0, int c, int rowblk0,
+                                                  const PotrfFwd& f, double* sZ, double* sR, int& fail) {
+  constexpr int V = PANEL ? (SPLIT == 1 ? 1 : 2) : 0;
+  constexpr bool PIV = OV && W == 0;  // this wave factors pivot block 0
+  constexpr int NCC = pre_count(kPreCC[OV][V][W], 5);
+  constexpr int IC0 = kPreIC[OV][V][W][0], NIC = kPreIC[OV][V][W][1];
+  constexpr int RB0 = IC0 / 4, NRB = NIC > 0 ? (IC0 + NIC - 1) / 4 - RB0 + 1 : 0;  // its A_ic row blocks
+  constexpr int RBF = kFoldRB[OV][V][W];
+  constexpr int NRI = 8 / SPLIT;  // double2 loads of L_i per thread (64 / SPLIT rows)
+  static_assert(SPLIT == 1 || SPLIT == 2, "panel split");
   const int t = threadIdx.x, lane = t & 63;
   const int g = lane >> 4, cl = lane & 15;
   double2 rl[8], ri[NRI];
-  d4 acc_cc[NCC], acc_ic[NIC];
-  // forward fold: z_{c-1} (-> LDS sZ) and this lane's old right-hand sides (row 16 RB + cl of the workgroup's rows,
+  d4 acc_cc[NCC], acc_ic[NIC > 0 ? NIC : 1];
+  // forward fold: z_{c-1} (-> LDS sZ) and this lane's old right-hand sides (row 16 RBF + cl of the workgroup's rows,
   // which start at global row rowblk0)
   double2 zv = make_double2(0.0, 0.0);
   double rold[NR > 0 ? NR : 1];
-  const int frow = rowblk0 + 16 * RB + cl;
   if constexpr (NR > 0) {
     if (t < 32 * NR) zv = *reinterpret_cast<const double2*>(f.z + (int64_t)(c - 1) * NB * NR + 2 * t);
+    if constexpr (RBF >= 0) {
+      const int frow = rowblk0 + 16 * RBF + cl;
 #pragma unroll
-    for (int rr = 0; rr < NR; ++rr)
-      rold[rr] = (g != 0 || !FOLD_ROWS) ? 0.0 : (c == 1 ? fwd_y(f, frow, rr) : f.r[(int64_t)frow * NR + rr]);
+      for (int rr = 0; rr < NR; ++rr)
+        rold[rr] = g != 0 ? 0.0 : (c == 1 ? fwd_y(f, frow, rr) : f.r[(int64_t)frow * NR + rr]);
+    }
   }
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -220,18 +254,22 @@ __device__ __forceinline__ void update_eager_wave(const double* __restrict__ Acc
     rl[q] = *reinterpret_cast<const double2*>(Lc + (int64_t)r * lda + cc);
     if (PANEL && q < NRI) ri[q] = *reinterpret_cast<const double2*>(Li + (int64_t)r * lda + cc);
   }
+  if constexpr (PIV) {
 #pragma unroll
-  for (int b = 0; b < NCC; ++b) {
-    const int bi = kLowerBlk[W + 4 * b][0], bj = kLowerBlk[W + 4 * b][1];
+    for (int q = 0; q < 4; ++q) acc_cc[0][q] = Acc[(int64_t)(4 * g + q) * lda + cl];  // chol16's layout
+  } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) acc_cc[b][q] = Acc[(int64_t)(16 * bi + g + 4 * q) * lda + 16 * bj + cl];
+    for (int b = 0; b < NCC; ++b) {
+      const int bi = kLowerBlk[kPreCC[OV][V][W][b]][0], bj = kLowerBlk[kPreCC[OV][V][W][b]][1];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc_cc[b][q] = Acc[(int64_t)(16 * bi + g + 4 * q) * lda + 16 * bj + cl];
+    }
   }
-  if (PANEL) {
 #pragma unroll
-    for (int j = 0; j < NIC; ++j)
+  for (int e = 0; e < NIC; ++e)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc_ic[j][q] = Aic[(int64_t)(16 * RB + g + 4 * q) * lda + 16 * (JB0 + j) + cl];
-  }
+    for (int q = 0; q < 4; ++q)
+      acc_ic[e][q] = Aic[(int64_t)(16 * ((IC0 + e) >> 2) + g + 4 * q) * lda + 16 * ((IC0 + e) & 3) + cl];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const int e = (t + q * WG) * 2, r = e >> 6, cc = e & 63;
@@ -244,69 +282,81 @@ __device__ __forceinline__ void update_eager_wave(const double* __restrict__ Acc
   __syncthreads();
   GPX_EAGER_STAMP(c, rowblk0, 0);
   // k in chunks of 16: one batch of fragment reads (the four L_c row blocks serve as the B operand of every block and as
-  // the A operand of the A_cc blocks; L_i's row block W is A_ic's A operand), then the chunk's MFMAs, independent
-  // across blocks
+  // the A operand of the A_cc blocks; L_i's row blocks are the A_ic blocks' A operands), then the chunk's MFMAs
   const int m = lane & 15, kq = lane >> 4;
-  // forward fold: r_i -= L_{i,c-1} z_{c-1} on the wave's 16 rows, from the L fragments the MFMAs read anyway (row block
-  // W of L_i, or of L_c for p = 0): lane (m, kq) sums k = kq mod 4, its FMAs issue between the chunk's MFMAs
+  const int mp = 4 * (m & 3) + (m >> 2);  // the pivot wave's A-operand row order
   double part[NR > 0 ? NR : 1];
 #pragma unroll
   for (int rr = 0; rr < (NR > 0 ? NR : 1); ++rr) part[rr] = 0.0;
 #pragma unroll
   for (int kc = 0; kc < NB; kc += 16) {
-    double fc[4][4], fi[4];
+    double fc[4][4], fi[NRB > 0 ? NRB : 1][4], fp[4], ff[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) fc[jb][s] = sA[(16 * jb + m) * LD64 + kc + 4 * s + kq];
-      if (PANEL) fi[s] = sP[(16 * RB + m) * LD64 + kc + 4 * s + kq];
+      if constexpr (PIV) fp[s] = sA[mp * LD64 + kc + 4 * s + kq];
+#pragma unroll
+      for (int i = 0; i < NRB; ++i) fi[i][s] = sP[(16 * (RB0 + i) + m) * LD64 + kc + 4 * s + kq];
+      if constexpr (NR > 0 && RBF >= 0) ff[s] = PANEL ? sP[(16 * RBF + m) * LD64 + kc + 4 * s + kq] : fc[RBF][s];
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      if (PANEL) {
 #pragma unroll
-        for (int j = 0; j < NIC; ++j) acc_ic[j] = mfma_sub(fi[s], fc[JB0 + j][s], acc_ic[j]);
+      for (int e = 0; e < NIC; ++e)
+        acc_ic[e] = mfma_sub(fi[((IC0 + e) >> 2) - RB0][s], fc[(IC0 + e) & 3][s], acc_ic[e]);
+      if constexpr (PIV) {
+        acc_cc[0] = mfma_sub(fp[s], fc[0][s], acc_cc[0]);
+      } else {
+#pragma unroll
+        for (int b = 0; b < NCC; ++b)
+          acc_cc[b] = mfma_sub(fc[kLowerBlk[kPreCC[OV][V][W][b]][0]][s], fc[kLowerBlk[kPreCC[OV][V][W][b]][1]][s],
+                               acc_cc[b]);
       }
+      if constexpr (NR > 0 && RBF >= 0) {
 #pragma unroll
-      for (int b = 0; b < NCC; ++b)
-        acc_cc[b] = mfma_sub(fc[kLowerBlk[W + 4 * b][0]][s], fc[kLowerBlk[W + 4 * b][1]][s], acc_cc[b]);
-      if constexpr (NR > 0 && FOLD_ROWS) {
-        const double lv = PANEL ? fi[s] : fc[W][s];
-#pragma unroll
-        for (int rr = 0; rr < NR; ++rr) part[rr] = fma(lv, sZ[(kc + 4 * s + kq) * NR + rr], part[rr]);
+        for (int rr = 0; rr < NR; ++rr) part[rr] = fma(ff[s], sZ[(kc + 4 * s + kq) * NR + rr], part[rr]);
       }
     }
   }
-  if constexpr (NR > 0 && FOLD_ROWS) {
+  if constexpr (NR > 0 && RBF >= 0) {
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr) part[rr] = rowsum4(part[rr]);
     if (g == 0) {
 #pragma unroll
-      for (int rr = 0; rr < NR; ++rr) {
-        sR[(16 * RB + cl) * NR + rr] = rold[rr] - part[rr];  // stored to global memory at the workgroup's end
-      }
+      for (int rr = 0; rr < NR; ++rr) sR[(16 * RBF + cl) * NR + rr] = rold[rr] - part[rr];
     }
   }
-  __syncthreads();  // every wave's operand reads done: sA / sP take the results
+  Blk16 bk;
+  if constexpr (PIV) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bk.a[q] = acc_cc[0][q];
+    fail = chol16_regs(bk);  // F of pivot block 0, under waves 1-3's MFMAs
+  }
+  __syncthreads();  // every wave's operand reads done: sA / sP take the results (and L_00, D_0)
   GPX_EAGER_STAMP(c, rowblk0, 1);
+  if constexpr (PIV) {
+    chol16_store<LDD>(bk, sA, sD0, 0);
+  } else {
 #pragma unroll
-  for (int b = 0; b < NCC; ++b) store_block16(sA, 16 * kLowerBlk[W + 4 * b][0], 16 * kLowerBlk[W + 4 * b][1], acc_cc[b]);
-  if (PANEL) {
+    for (int b = 0; b < NCC; ++b)
+      store_block16(sA, 16 * kLowerBlk[kPreCC[OV][V][W][b]][0], 16 * kLowerBlk[kPreCC[OV][V][W][b]][1], acc_cc[b]);
 #pragma unroll
-    for (int j = 0; j < NIC; ++j) store_block16(sP, 16 * RB, 16 * (JB0 + j), acc_ic[j]);
+    for (int e = 0; e < NIC; ++e) store_block16(sP, 16 * ((IC0 + e) >> 2), 16 * ((IC0 + e) & 3), acc_ic[e]);
   }
 }
 
-template <bool PANEL, int NR, int SPLIT>
+// OV: the overlapped lists (pivot block 0 factored on return: L_00 in sA, D_0 in sD0, fail = its failing pivot or -1)
+template <bool OV, bool PANEL, int NR, int SPLIT>
 __device__ __forceinline__ void update_eager(const double* __restrict__ Acc, const double* __restrict__ Aic,
                                              const double* __restrict__ Lc, const double* __restrict__ Li, int64_t lda,
-                                             double* sA, double* sP, int c, int rowblk0, const PotrfFwd& f, double* sZ,
-                                             double* sR) {
+                                             double* sA, double* sP, double* sD0, int c, int rowblk0,
+                                             const PotrfFwd& f, double* sZ, double* sR, int& fail) {
   switch (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) {  // wave-uniform: compile-time block lists per wave
-    case 0: update_eager_wave<0, PANEL, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
-    case 1: update_eager_wave<1, PANEL, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
-    case 2: update_eager_wave<2, PANEL, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
-    default: update_eager_wave<3, PANEL, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, c, rowblk0, f, sZ, sR); break;
+    case 0: update_eager_wave<0, OV, PANEL, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, sD0, c, rowblk0, f, sZ, sR, fail); break;
+    case 1: update_eager_wave<1, OV, PANEL, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, sD0, c, rowblk0, f, sZ, sR, fail); break;
+    case 2: update_eager_wave<2, OV, PANEL, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, sD0, c, rowblk0, f, sZ, sR, fail); break;
+    default: update_eager_wave<3, OV, PANEL, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, sD0, c, rowblk0, f, sZ, sR, fail); break;
   }
 }
 
@@ -357,7 +407,7 @@ __device__ __forceinline__ void load_tile_lds(const double* __restrict__ G, int6
 template <int NR, int SPLIT>
 __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, int c, int p, int h, int nblk, int c0,
                                            double* __restrict__ Dinv, int32_t* __restrict__ info, double* lds,
-                                           const PotrfFwd& f, int32_t* __restrict__ done = nullptr) {
+                                           const PotrfFwd& f, bool ov) {
   constexpr int PROWS = NB / SPLIT;  // rows of A_ic this workgroup owns
   double* sA = lds;             // A_cc -> L_cc
   double* sP = sA + NB * LD64;  // A_ic -> L_ic (p > 0)
@@ -379,6 +429,8 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
   const double* Acc = A + (int64_t)c * NB * lda + (int64_t)c * NB;
   double* Aic = A + (int64_t)row0 * lda + (int64_t)c * NB;
   if (t == 0) s_tdone = 0;
+  int fail = -1;
+  bool f0 = false;  // pivot block 0 already factored by the pre-update (wave 0)
   if (c > 0) {
     // the updates of block columns c0 .. c-1 not yet applied to this column, on the two tiles this workgroup
     // factors (K = 64 (c - c0))
@@ -386,10 +438,18 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
     const double* Lc = A + (int64_t)c * NB * lda + (int64_t)c0 * NB;
     const double* Li = A + (int64_t)row0 * lda + (int64_t)c0 * NB;
     if (kk == NB) {
-      if (panel)
-        update_eager<true, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, c, row0, f, sZ, sR);
-      else
-        update_eager<false, NR, 1>(Acc, Aic, Lc, Li, lda, sA, sP, c, c * NB, f, sZ, sR);
+      if (ov) {
+        if (panel)
+          update_eager<true, true, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, sDb, c, row0, f, sZ, sR, fail);
+        else
+          update_eager<true, false, NR, 1>(Acc, Aic, Lc, Li, lda, sA, sP, sDb, c, c * NB, f, sZ, sR, fail);
+        f0 = true;
+      } else {
+        if (panel)
+          update_eager<false, true, NR, SPLIT>(Acc, Aic, Lc, Li, lda, sA, sP, sDb, c, row0, f, sZ, sR, fail);
+        else
+          update_eager<false, false, NR, 1>(Acc, Aic, Lc, Li, lda, sA, sP, sDb, c, c * NB, f, sZ, sR, fail);
+      }
     } else {
       // (never split: the host splits panels only in schedules whose panels apply one column)
       // (the host folds the forward substitution only into schedules whose panels apply one column: kk == NB)
@@ -429,18 +489,17 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
   auto publish = [&]() {
     if ((t & 63) == 0) __hip_atomic_fetch_add(&s_tdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   };
-  int fail = -1;
   for (int s = 0; s < 4; ++s) {
     const int o = 16 * s;
     double* D = sDb + (s & 1) * 16 * LDD;
-    if (w == 0) {
+    if (w == 0 && (s > 0 || !f0)) {
       // (4-pivot blocks on v_mfma_f64_16x16x4, tools/chol16_probe.hip: correct, but measured slower inside the panel,
       // potrf 1.89 vs 1.76 ms at n = 4096: ~75 instructions per pivot and MFMA / ds_bpermute latency on the chain)
       const int f = chol16<LDD>(sA, D, o);
       if (f >= 0 && fail < 0) fail = o + f;
     }
     GPX_PANEL_STAMP(1 + 3 * s);
-    __syncthreads();  // publishes L_ss and D_ss
+    if (s > 0 || !f0) __syncthreads();  // publishes L_ss and D_ss (step 0 after a pre-update: published already)
     if (w == 0) {
       // Critical path, no barrier: T and U of the next pivot block, then straight on to its F.
       if (s + 1 < nrow) tsolve(s + 1, D, o);  // at s = 3 this is the first panel row block
@@ -492,11 +551,6 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
   if constexpr (NR > 0) {
     if (c > 0)
       for (int e = t; e < PROWS * NR; e += WG) f.r[(int64_t)row0 * NR + e] = sR[e];
-  }
-  if (done) {  // decoupled trailing update: publish "PROWS more rows of column c" (write-through stores, drained)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) __hip_atomic_fetch_add(done + c, PROWS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -617,15 +671,12 @@ struct StepPlan {
   int npanel, nlook, ntrail, c0, look_a, cfirst, k0, flush;
   int tbase, xmap;  // first trailing workgroup (a multiple of 8 when xmap: XCD-chunked tile order), tile order
   int split;        // panel row blocks c+1.. split into 1, 2 or 4 workgroups (panel workgroup b > 0: p = 1 + (b-1) / split)
-  int near;         // > 0: decoupled trailing update, only tile columns closer than `near` block columns (ntrail of them)
-  int32_t* sync;    // decoupled trailing update: the sync words (potrf_side_kernel), else nullptr
-  unsigned limit;   // their bounded polls (Context::spin_limit)
+  int overlap;      // the panels' first pivot block factored under their pre-update (update_eager OV)
 };
 
 // slots > 0: the co-resident workgroup slots a problem may fill (two per CU, shared by a batch); the panel row blocks are
 // split in 2 (StepPlan::split) when the panels apply exactly one column and the split launch still fits the slots.
-inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush, int xmap = 0, int slots = 0,
-                          int near = 0) {
+inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush, int xmap = 0, int slots = 0) {
   StepPlan s;
   s.npanel = nblk - c;
   s.split = 1;
@@ -646,14 +697,6 @@ inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush,
   const int M = (flush && m > 0) ? (m + 1) / 2 : 0;
   s.ntrail = M * (M + 1) / 2;
   s.xmap = xmap;
-  s.near = 0;
-  s.sync = nullptr;
-  s.limit = 0;
-  if (near > 0 && mode == 0 && flush && c - last_flush == 1) {
-    s.near = near;
-    s.ntrail = 0;
-    for (int J = 0; J < M && nblk - 2 * M + 2 * J - c < near; ++J) s.ntrail += M - J;
-  }
   const bool eager = mode == 1 || c == 0 || c - last_flush == 1;
   if (slots > 0 && eager && s.npanel > 1) {
     for (int sp = 2; sp >= 2; sp >>= 1) {  // split 4 measured slower at n = 4096 (potrf 1.48 vs 1.46 ms), equal below
@@ -667,103 +710,10 @@ inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush,
     }
   }
   s.tbase = xmap ? (s.npanel + s.nlook + 7) & ~7 : s.npanel + s.nlook;  // padding workgroups exit at once
+  // the overlapped pre-update shortens the panel chain but slows launches whose trailing workgroups do not all fit
+  // the co-resident slots at once
+  s.overlap = slots > 0 && s.tbase + s.ntrail <= slots;
   return s;
-}
-
-// ---- decoupled trailing update (GPX_OPT_POTRF_DECOUPLE, eager schedule only) -------------------------------------
-// The flush of launch c covers only the NEAR 128-tile columns (origin q0 - c < D); a persistent side kernel on a
-// second stream applies every earlier column to the FAR tiles as soon as the panels have published it, so the step
-// launches on the critical path stop paying for the bulk of the trailing matrix.  Tile (r0, q0) becomes near at
-// launch cn = q0 - D + 1: the side kernel owns its columns 0 .. cn - 2 (in SIDE_CHUNK-column products), the step
-// launches cn, cn+1, ... one column each.  The chunking is fixed, so the factor is deterministic; it differs from the
-// eager schedule's (one column per product everywhere) by rounding only.
-// Sync words (zeroed on the stream before the factorisation): done[k], k < nblk = rows of column k the panel
-// workgroups of launch k have stored (complete at (nblk - 1 - k) * 64); ver[(r0/2) * (nblk/2) + q0/2] = the columns the
-// side kernel has applied to the tile.  Producers: write-through stores, s_waitcnt vmcnt(0), barrier, one relaxed
-// agent-scope atomic (cdna_hip_programming.md §6, form R1); consumers: one lane polls, acquires, then the barrier.
-constexpr int SIDE_CHUNK = 8;  // columns per side-kernel pass over a tile (K = 512)
-
-// one lane: bounded poll until *w >= v; false on timeout or when the factorisation was aborted (info != 0)
-__device__ __forceinline__ bool poll_at_least(int32_t* w, int32_t v, int32_t* info, unsigned limit) {
-  for (unsigned spins = 0;; ++spins) {
-    if (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= v) break;
-    if (spins >= limit ||
-        ((spins & 63) == 63 && __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0))
-      return false;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  (void)__hip_atomic_load(w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-  return true;
-}
-
-// Near trailing workgroup `p` of launch c (tile columns in order, rows within a column): a tile that becomes near at
-// this launch first waits for the side kernel's columns.
-__device__ __forceinline__ void near_role(double* __restrict__ A, int64_t lda, int c, int nblk, const StepPlan& s, int p,
-                                          int32_t* __restrict__ info, double* lds) {
-  __shared__ int s_ok;
-  const int M = (nblk - s.cfirst + 1) / 2, c0 = nblk - 2 * M;
-  int J = 0;
-  while (p >= M - J) {
-    p -= M - J;
-    ++J;
-  }
-  const int r0 = c0 + 2 * (J + p), q0 = c0 + 2 * J, cn = q0 - s.near + 1;
-  if (c == cn && cn >= 2) {
-    if (threadIdx.x == 0) {
-      s_ok = poll_at_least(s.sync + nblk + (r0 >> 1) * (nblk >> 1) + (q0 >> 1), cn - 1, info, s.limit);
-      if (!s_ok) atomicCAS(info, 0, (int32_t)GPX_INFO_TIMEOUT);
-    }
-    __syncthreads();
-    if (!s_ok) return;
-  }
-  trailing_tile_at(A, lda, c, s.k0, s.cfirst, r0, q0, lds);
-}
-
-// The far tiles (q0 >= D + 1, in q0 order, dealt round-robin to the workgroups; one workgroup per CU): pass after pass,
-// the next SIDE_CHUNK columns of every owned tile, each once the panels have published its last column.
-__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
-potrf_side_kernel(double* __restrict__ A, int64_t lda, int nblk, int D, int32_t* __restrict__ sync,
-                  int32_t* __restrict__ info, unsigned limit) {
-  __shared__ __attribute__((aligned(16))) double lds[Tile128::LDS_DOUBLES];
-  __shared__ int s_ok;
-  const int qmin = (D + 2) & ~1;  // the smallest even q0 >= D + 1
-  int ntile = 0;
-  for (int q0 = qmin; q0 < nblk; q0 += 2) ntile += (nblk - q0) >> 1;
-#pragma unroll 1
-  for (int kb = 0;; kb += SIDE_CHUNK) {
-    bool any = false;
-#pragma unroll 1
-    for (int tix = blockIdx.x; tix < ntile; tix += gridDim.x) {
-      int q0 = qmin, rem = tix;
-      while (rem >= (nblk - q0) >> 1) {
-        rem -= (nblk - q0) >> 1;
-        q0 += 2;
-      }
-      const int r0 = q0 + 2 * rem, kend = q0 - D;  // this kernel's columns: 0 .. kend - 1
-      if (kb >= kend) continue;
-      any = true;
-      const int ke = min(kb + SIDE_CHUNK, kend);
-      if (threadIdx.x == 0) {
-        s_ok = poll_at_least(sync + ke - 1, (nblk - ke) * NB, info, limit);
-        if (!s_ok) atomicCAS(info, 0, (int32_t)GPX_INFO_TIMEOUT);
-      }
-      __syncthreads();
-      if (!s_ok) return;
-      // (A and lda opaque per tile: the tile's address arithmetic is not hoisted out of these loops, whose live-through
-      // values the 128x128 accumulators leave no registers for; what still spills is saved once per kernel and
-      // reloaded once per tile, one reload per k-tile of 64 MFMAs)
-      double* At = A;
-      int64_t ldt = lda;
-      asm volatile("" : "+s"(At), "+s"(ldt));
-      trailing_tile_at(At, ldt, ke, kb, 0, r0, q0, lds);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0)
-        __hip_atomic_store(sync + nblk + (r0 >> 1) * (nblk >> 1) + (q0 >> 1), ke, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (!any) return;
-  }
 }
 
 // NR: 0 = no forward fold, else its right-hand-side row length (one instantiation each: the fold's registers stay out
@@ -788,13 +738,11 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, StepPlan
       f.z += blockIdx.y * f.sb;
     }
     if (s.split == 2 && b > 0)
-      panel_role<NR, 2>(A, lda, c, 1 + ((b - 1) >> 1), (b - 1) & 1, nblk, s.c0, Dinv, info, lds, f, s.sync);
+      panel_role<NR, 2>(A, lda, c, 1 + ((b - 1) >> 1), (b - 1) & 1, nblk, s.c0, Dinv, info, lds, f, s.overlap);
     else
-      panel_role<NR, 1>(A, lda, c, b, 0, nblk, s.c0, Dinv, info, lds, f, s.sync);
+      panel_role<NR, 1>(A, lda, c, b, 0, nblk, s.c0, Dinv, info, lds, f, s.overlap);
   } else if (role == 1)
     lookahead_role(A, lda, c, s.look_a, b - s.npanel, lds);
-  else if (s.near > 0)
-    near_role(A, lda, c, nblk, s, b - s.tbase, info, lds);
   else
     trailing_role(A, lda, c, nblk, s.k0, s.cfirst, b - s.tbase, s.ntrail, s.xmap, lds);
   GPX_STEP_STAMP(role, c, b, 1);
@@ -858,21 +806,14 @@ static int potrf_mode(const Context* ctx, int nblk) {
   return nblk > 64 ? 1 : 0;
 }
 
-// Near distance D of the decoupled trailing update (0 = off): eager schedule (mode 0, g = 1), one problem.  Off by
-// size until measured faster (GPX_OPT_POTRF_DECOUPLE turns it on).
-static int potrf_decouple(const Context* ctx, int nblk, int mode, int batch) {
-  if (batch != 1 || mode != 0 || potrf_lazy(ctx, nblk) != 1 || ctx->potrf_decouple <= 0) return 0;
-  return ctx->potrf_decouple < nblk ? ctx->potrf_decouple : 0;  // D >= nblk: every tile is near
-}
-
 // The plan of every launch c < cend (flush launches: c >= 1 and at least one interval after the previous flush).
 template <typename F>
-static void for_each_step(const Context* ctx, int nblk, int mode, int cend, int slots, F&& f, int near = 0) {
+static void for_each_step(const Context* ctx, int nblk, int mode, int cend, int slots, F&& f) {
   const int g = potrf_lazy(ctx, nblk);
   int last = 0;
   for (int c = 0; c < cend; ++c) {
     const bool flush = c >= 1 && c - last >= g;
-    f(c, step_plan(c, nblk, mode, last, flush, 1, slots, near));
+    f(c, step_plan(c, nblk, mode, last, flush, 1, slots));
     if (flush) last = c;
   }
 }
@@ -889,52 +830,11 @@ static int potrf_slots(Context* ctx, int batch) {
   return 2 * ctx->cu_count / (batch > 0 ? batch : 1);
 }
 
-// The decoupled update's side stream, events and sync words (created on first use, kept by the handle).
-static hipError_t side_resources(Context* ctx, size_t bytes) {
-  hipError_t e = hipSuccess;
-  if (!ctx->side_stream) e = hipStreamCreateWithFlags(&ctx->side_stream, hipStreamNonBlocking);
-  if (e == hipSuccess && !ctx->ev_fork) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
-  if (e == hipSuccess && !ctx->ev_join) e = hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming);
-  if (e == hipSuccess && ctx->sync_bytes < bytes) {
-    if (ctx->sync_buf) {
-      e = hipStreamSynchronize(ctx->stream);  // an earlier factorisation may still use the old words
-      if (e == hipSuccess) e = hipFree(ctx->sync_buf);
-      ctx->sync_buf = nullptr;
-      ctx->sync_bytes = 0;
-    }
-    if (e == hipSuccess) e = hipMalloc(&ctx->sync_buf, bytes);
-    if (e == hipSuccess) ctx->sync_bytes = bytes;
-  }
-  return e;
-}
-
-static hipError_t launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info,
-                               const Batch& bt, int cbeg, int cend, const PotrfFwd& f = PotrfFwd()) {
+static void launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
+                         int cbeg, int cend, const PotrfFwd& f = PotrfFwd()) {
   const int mode = potrf_mode(ctx, nblk);
-  int slots = potrf_slots(ctx, bt.count);
-  const int D = slots > 0 && cbeg == 0 && cend == nblk ? potrf_decouple(ctx, nblk, mode, bt.count) : 0;
-  int32_t* sync = nullptr;
-  if (D > 0) {
-    const size_t bytes = (size_t)(nblk + (nblk / 2) * (nblk / 2)) * sizeof(int32_t);
-    hipError_t e = side_resources(ctx, bytes);
-    if (e == hipSuccess) e = hipMemsetAsync(ctx->sync_buf, 0, bytes, ctx->stream);
-    if (e == hipSuccess) e = hipEventRecord(ctx->ev_fork, ctx->stream);
-    if (e == hipSuccess) e = hipStreamWaitEvent(ctx->side_stream, ctx->ev_fork, 0);
-    if (e != hipSuccess) return e;
-    sync = ctx->sync_buf;
-    int ntile = 0;
-    for (int q0 = (D + 2) & ~1; q0 < nblk; q0 += 2) ntile += (nblk - q0) / 2;
-    const int grid = ntile < slots / 2 ? ntile : slots / 2;  // one workgroup per CU
-    if (grid > 0)
-      potrf_side_kernel<<<grid, WG, 0, ctx->side_stream>>>(A, lda, nblk, D, sync, info, ctx->spin_limit);
-    e = hipEventRecord(ctx->ev_join, ctx->side_stream);
-    if (e != hipSuccess) return e;
-    slots /= 2;  // the other slot of every CU is the step launches'
-  }
-  for_each_step(ctx, nblk, mode, cend, slots, [&](int c, StepPlan s) {
+  for_each_step(ctx, nblk, mode, cend, potrf_slots(ctx, bt.count), [&](int c, const StepPlan& s) {
     if (c < cbeg) return;
-    s.sync = sync;
-    s.limit = ctx->spin_limit;
     const dim3 grid(s.tbase + s.ntrail, bt.count);
     if (!f.r)
       potrf_step_kernel<0><<<grid, WG, 0, ctx->stream>>>(A, lda, c, nblk, s, Dinv, info, 0, bt.k, bt.dinv, f);
@@ -942,8 +842,7 @@ static hipError_t launch_steps(Context* ctx, int nblk, double* A, int64_t lda, d
       potrf_step_kernel<1><<<grid, WG, 0, ctx->stream>>>(A, lda, c, nblk, s, Dinv, info, 0, bt.k, bt.dinv, f);
     else
       potrf_step_kernel<GPX_MAX_RHS><<<grid, WG, 0, ctx->stream>>>(A, lda, c, nblk, s, Dinv, info, 0, bt.k, bt.dinv, f);
-  }, D);
-  return D > 0 ? hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0) : hipSuccess;
+  });
 }
 
 static void launch_dinv(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
@@ -973,8 +872,7 @@ hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* 
     f.n = fr->n;
     f.mean = fr->mean;
   }
-  const hipError_t es = launch_steps(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, f);
-  if (es != hipSuccess) return es;
+  launch_steps(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, f);
   launch_dinv(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, W, ldw);
   const hipError_t e = hipGetLastError();
   if (e == hipSuccess && z_done && f.r) *z_done = true;

@@ -203,7 +203,7 @@ class GPEngine:
     # -- fit --------------------------------------------------------------------------------------
     def set_option(self, name: str, value: int) -> None:
         """Per-handle tuning / diagnostic option (include/gpx.h GPX_OPT_*: spin_limit, sweep_fused,
-        gram_split, potrf_lazy, potrf_mode, potrf_decouple)."""
+        gram_split, potrf_lazy, potrf_mode)."""
         self._check(self.lib.gpx_set_option(self.handle, _capi.OPTIONS[name], int(value)))
 
     def get_option(self, name: str) -> int:

@@ -138,18 +138,14 @@ size_t gpx_acq_params_size(void);
  *  GPX_OPT_SWEEP_FUSED     1 (default) the fused small-n sweep where it applies (padded n <= 256), 0 the K* + trmm path
  *  GPX_OPT_GRAM_SPLIT      0 by size (default), else 1, 2 or 4 workgroups per 64x64 Gram tile
  *  GPX_OPT_POTRF_LAZY      multi-launch schedule: 0 by size (default), else flush the trailing update every g columns
- *  GPX_OPT_POTRF_MODE      multi-launch schedule: -1 by size (default), 0 eager panels, 1 lookahead panels
- *  GPX_OPT_POTRF_DECOUPLE  eager schedule, single problem: 0 off, D >= 2 the trailing tiles D or more block columns
- *                          right of the panel are updated by a concurrent kernel on an internal stream (K <= 512
- *                          chunks as the panels publish columns), -1 by size (default) */
+ *  GPX_OPT_POTRF_MODE      multi-launch schedule: -1 by size (default), 0 eager panels, 1 lookahead panels */
 enum {
   GPX_OPT_SPIN_LIMIT = 0,
   GPX_OPT_SWEEP_FUSED = 1,
   GPX_OPT_GRAM_SPLIT = 2,
   GPX_OPT_POTRF_LAZY = 3,
   GPX_OPT_POTRF_MODE = 4,
-  GPX_OPT_POTRF_DECOUPLE = 5,
-  GPX_OPT_COUNT = 6
+  GPX_OPT_COUNT = 5
 };
 gpx_status gpx_set_option(gpx_handle h, int32_t option, int64_t value);
 gpx_status gpx_get_option(gpx_handle h, int32_t option, int64_t* value_host);

@@ -88,14 +88,14 @@ def test_batched_timeout_names_the_problem(engine):
 
 def test_options_roundtrip_and_validation(engine):
     for name, value in (("spin_limit", 12345), ("sweep_fused", 0), ("gram_split", 2),
-                        ("potrf_lazy", 3), ("potrf_mode", 1), ("potrf_decouple", 4)):
+                        ("potrf_lazy", 3), ("potrf_mode", 1)):
         old = engine.get_option(name)
         engine.set_option(name, value)
         assert engine.get_option(name) == value
         engine.set_option(name, old)
         assert engine.get_option(name) == old
     for name, bad in (("spin_limit", -1), ("sweep_fused", 2), ("gram_split", 3),
-                      ("potrf_lazy", 17), ("potrf_mode", 2), ("potrf_decouple", 1), ("potrf_decouple", -2)):
+                      ("potrf_lazy", 17), ("potrf_mode", 2)):
         with pytest.raises(GPXError) as e:
             engine.set_option(name, bad)
         assert e.value.status == _capi.GPX_INVALID_ARG
@@ -225,34 +225,3 @@ def test_fit_beside_a_long_kernel_on_another_stream(engine):
             torch.cuda.synchronize()
             outcomes.append("timeout")
     assert outcomes.count("ok") >= 1, outcomes
-
-
-@pytest.mark.parametrize("n", [1000, 4096])
-@pytest.mark.parametrize("near", [2, 5])
-def test_decoupled_trailing_update(engine, n, near):
-    """GPX_OPT_POTRF_DECOUPLE: the far trailing tiles updated by a concurrent side kernel (SIDE_CHUNK columns per
-    product) while the step launches flush only the near tile columns.  The factor equals the default schedule's to
-    rounding (1e-12 relative: only the grouping of each tile's K sum differs), is deterministic run to run, alpha meets
-    the oracle, and a failing pivot deep in the matrix is still reported at its row."""
-    d = 8
-    X, y = O.synthetic_problem(n, d, 70)
-    kp, op = pair("rbf", d, noise=1e-4)
-    st0 = engine.fit(t(X), t(y), kp)
-    L0 = np.tril(st0.L.cpu().numpy())
-    engine.set_option("potrf_decouple", near)
-    try:
-        st1 = engine.fit(t(X), t(y), kp)
-        L1 = np.tril(st1.L.cpu().numpy())
-        st2 = engine.fit(t(X), t(y), kp)
-        np.testing.assert_array_equal(np.tril(st2.L.cpu().numpy()), L1)
-        assert np.abs(L1 - L0).max() <= 1e-12 * np.abs(L0).max()
-        ar = O.fit(X, y, op).alpha.reshape(-1)
-        a = st1.alpha.cpu().numpy().reshape(-1)
-        assert np.abs(a[:n] - ar).max() <= 1e-8 * np.abs(ar).max()
-        K = engine.gram(t(X), kp)
-        piv = n // 2 + 37
-        K[piv, piv] = -1.0
-        _, info = engine.potrf(K, n)
-        assert int(info.item()) == piv + 1
-    finally:
-        engine.set_option("potrf_decouple", -1)

@@ -63,6 +63,19 @@ int main(int argc, char** argv) {
     CK(hipExtMallocWithFlags((void**)&A, hA.size() * 8, amode));
   CK(hipMalloc(&Dv, (size_t)2 * nblk * 4096 * 8));
   CK(hipMalloc(&info, 4));
+  // argv[3]: right-hand sides of a folded forward substitution (0: the plain factorisation; 1: a fit's, NR = 1)
+  const int nrhs = argc > 3 ? atoi(argv[3]) : 0;
+  double *Y, *fbuf;
+  CK(hipMalloc(&Y, (size_t)npad * 8 * 8));
+  CK(hipMalloc(&fbuf, (size_t)2 * npad * GPX_MAX_RHS * 8));
+  CK(hipMemset(Y, 0, (size_t)npad * 8 * 8));
+  ForwardRhs fr;
+  fr.Y = Y;
+  fr.ldy = nrhs > 0 ? nrhs : 1;
+  fr.nrhs = nrhs > 0 ? nrhs : 1;
+  fr.n = n;
+  fr.buf = fbuf;
+  bool zdone = false;
   Context ctx;
   Batch bt{1, 0, 0, 0};
   hipEvent_t e0, e1;
@@ -78,7 +91,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_tend), zeros.data(), 2048));
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0, 0));
-    CK(launch_potrf(&ctx, npad, A, npad, Dv, info, bt, nullptr, 0));
+    CK(launch_potrf(&ctx, npad, A, npad, Dv, info, bt, nullptr, 0, nrhs > 0 ? &fr : nullptr, &zdone));
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     CK(hipEventElapsedTime(&ms, e0, e1));
