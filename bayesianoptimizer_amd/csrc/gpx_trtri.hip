@@ -31,12 +31,33 @@ __global__ void __launch_bounds__(WG) trtri_diag_kernel(const double* __restrict
   }
 }
 
+// Block order of the 128-tile levels (large n): one output tile per workgroup, heaviest k-range first (no long tile
+// left running alone at the end of a level), XCD-aware when the free index spans a multiple of 8 tiles: the
+// round-robin dispatch puts workgroups b, b+8, ... on one XCD, so XCD x takes the free tiles f = x (mod 8) and walks the
+// heavy index down, its resident workgroups sharing 8 free-operand panels through one L2 (the sweep product's order,
+// gpx_sweep.hip).  n = 16384, last level: T 9.24 -> 8.08 ms, W12 9.55 -> 8.68 ms against the paired order
+// (tools/trtri_bench.hip, profiles/r04_trtri_order_bench.log; same tiles, bit-identical); the whole inverse
+// 25.7 -> 23.6 ms.  The 64-tile levels keep the paired order (PAIRED: a workgroup takes the k-ranges of tile pair
+// (x, nt - 1 - x), so every workgroup does the same work; the XCD order measured 0.72 vs 0.66 ms at n = 4096).
+// nH / nF: tile counts of a full group; tiles past a partial last group exit.
+__device__ __forceinline__ void trtri_order(int b, int nH, int nF, bool heavy_high, int& H, int& F) {
+  int q;
+  if ((nF & 7) == 0) {
+    const int l = b >> 3, per = nF >> 3;
+    q = l / per;
+    F = 8 * (l % per) + (b & 7);
+  } else {
+    q = b / nF;
+    F = b % nF;
+  }
+  H = heavy_high ? nH - 1 - q : q;
+}
+
 // T_p = L21^T W22 for group p of level with half-size h blocks (TS x TS output tiles; TS = 64, or 128 for the big
 // levels of large n).  blockIdx.z = group + groups * problem.  The k-range of tile (rb, cb) is (cb + 1) * TS (W22
-// upper; its 128-aligned diagonal tiles have the strictly-lower 64-block zeroed by trtri_diag), so one workgroup
-// takes the column pair cb and nt2 - 1 - cb: every workgroup then does the same (nt2 + 1) * TS k-steps (the
-// unpaired form left the long tiles of the last level running alone: 291 us vs 176 us at n = 4096).
-template <int TS>
+// upper; its 128-aligned diagonal tiles have the strictly-lower 64-block zeroed by trtri_diag).  PAIRED: grid
+// (pairs, rows), column pair cb, nt2 - 1 - cb; else grid nt1^2, trtri_order with heavy index cb.
+template <int TS, bool PAIRED>
 __global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ L, int64_t ldl,
                                                      const double* __restrict__ W, int64_t ldw,
                                                      double* __restrict__ T, int h, int nblk, int groups, int64_t sl,
@@ -49,19 +70,16 @@ __global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ 
   T += prob * st;
   const int s1 = p * 2 * h, s2 = s1 + h;
   const int nb2 = min(2 * h, nblk - s1) - h;
+  if (nb2 <= 0) return;
   const int b1 = h * NB, b2 = nb2 * NB;
-  const int nt2 = b2 / TS;
-  const int rb = blockIdx.y;
-  if (nb2 <= 0 || (int)blockIdx.x >= (nt2 + 1) / 2) return;
+  const int nt1 = b1 / TS, nt2 = b2 / TS;
   const int64_t off1 = (int64_t)s1 * NB, off2 = (int64_t)s2 * NB;
   // T_p is b1 x b2 with row length b2; every group before the last is full (b2 = b1), so group p starts at
   // p*b1*b1 and the level's total sum_p b1*b2_p <= b1*(npad-b1) <= npad^2/4 fits the workspace.
   double* Tp = T + (int64_t)p * b1 * b1;
-  for (int pass = 0; pass < 2; ++pass) {
-    const int cb = pass == 0 ? (int)blockIdx.x : nt2 - 1 - (int)blockIdx.x;
-    if (pass == 1 && cb == (int)blockIdx.x) break;
-    const double* Ab = L + off2 * ldl + off1 + rb * TS;   // A(m=r,k=q) = L[off2+q][off1+r]
-    const double* Bb = W + off2 * ldw + off2 + cb * TS;   // B(k=q,n=c) = W[off2+q][off2+c]
+  auto tile_at = [&](int rb, int cb) {
+    const double* Ab = L + off2 * ldl + off1 + rb * TS;  // A(m=r,k=q) = L[off2+q][off1+r]
+    const double* Bb = W + off2 * ldw + off2 + cb * TS;  // B(k=q,n=c) = W[off2+q][off2+c]
     Tile tile;
     tile.run(Ab, ldl, Bb, ldw, 0, (cb + 1) * TS, smem);
 #pragma unroll
@@ -71,12 +89,24 @@ __global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ 
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           Tp[(int64_t)(rb * TS + Tile::row_of(i, r)) * b2 + cb * TS + Tile::col_of(j)] = tile.acc[i][j][r];
+  };
+  if constexpr (PAIRED) {
+    const int rb = blockIdx.y, x = blockIdx.x;
+    if (x >= (nt2 + 1) / 2) return;
+    tile_at(rb, x);
+    if (nt2 - 1 - x != x) {  // (run() ends with a barrier after its last LDS read)
+      tile_at(rb, nt2 - 1 - x);
+    }
+  } else {
+    int cb, rb;
+    trtri_order(blockIdx.x, nt1, nt1, true, cb, rb);
+    if (cb < nt2) tile_at(rb, cb);
   }
 }
 
-// W12 = -W11 T_p.  The k-range of tile (rb, cb) is [rb * TS, b1) (W11 upper): one workgroup takes the row pair
-// rb and nt1 - 1 - rb (same balancing as trtri_t_kernel).
-template <int TS>
+// W12 = -W11 T_p.  The k-range of tile (rb, cb) is [rb * TS, b1) (W11 upper).  PAIRED: grid (cols, pairs), row pair
+// rb, nt1 - 1 - rb; else grid nt1^2, trtri_order with heavy index rb (lightest last).
+template <int TS, bool PAIRED>
 __global__ void __launch_bounds__(WG) trtri_w_kernel(double* __restrict__ W, int64_t ldw, const double* __restrict__ T,
                                                      int h, int nblk, int groups, int64_t sw, int64_t st) {
   using Tile = MfmaTile<TS, TS, 16, false, true>;
@@ -86,16 +116,13 @@ __global__ void __launch_bounds__(WG) trtri_w_kernel(double* __restrict__ W, int
   T += prob * st;
   const int s1 = p * 2 * h, s2 = s1 + h;
   const int nb2 = min(2 * h, nblk - s1) - h;
+  if (nb2 <= 0) return;
   const int b1 = h * NB, b2 = nb2 * NB;
   const int nt1 = b1 / TS, nt2 = b2 / TS;
-  const int cb = blockIdx.x;
-  if (nb2 <= 0 || cb >= nt2 || (int)blockIdx.y >= (nt1 + 1) / 2) return;
   const int64_t off1 = (int64_t)s1 * NB, off2 = (int64_t)s2 * NB;
-  const double* Bb = T + (int64_t)p * b1 * b1 + cb * TS;          // B(k=q,n=c) = T[q][c], row length b2
-  for (int pass = 0; pass < 2; ++pass) {
-    const int rb = pass == 0 ? (int)blockIdx.y : nt1 - 1 - (int)blockIdx.y;
-    if (pass == 1 && rb == (int)blockIdx.y) break;
-    const double* Ab = W + (off1 + rb * TS) * ldw + off1;           // A(m=r,k=q) = W[off1+r][off1+q]
+  auto tile_at = [&](int rb, int cb) {
+    const double* Bb = T + (int64_t)p * b1 * b1 + cb * TS;  // B(k=q,n=c) = T[q][c], row length b2
+    const double* Ab = W + (off1 + rb * TS) * ldw + off1;   // A(m=r,k=q) = W[off1+r][off1+q]
     Tile tile;
     tile.run(Ab, ldw, Bb, b2, rb * TS, b1, smem);
     double* Wo = W + (off1 + rb * TS) * ldw + off2 + cb * TS;
@@ -104,8 +131,19 @@ __global__ void __launch_bounds__(WG) trtri_w_kernel(double* __restrict__ W, int
 #pragma unroll
       for (int j = 0; j < Tile::WN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Wo[(int64_t)Tile::row_of(i, r) * ldw + Tile::col_of(j)] = -tile.acc[i][j][r];
+        for (int r = 0; r < 4; ++r) Wo[(int64_t)Tile::row_of(i, r) * ldw + Tile::col_of(j)] = -tile.acc[i][j][r];
+  };
+  if constexpr (PAIRED) {
+    const int cb = blockIdx.x, y = blockIdx.y;
+    if (cb >= nt2 || y >= (nt1 + 1) / 2) return;
+    tile_at(y, cb);
+    if (nt1 - 1 - y != y) {  // (run() ends with a barrier after its last LDS read)
+      tile_at(nt1 - 1 - y, cb);
+    }
+  } else {
+    int rb, cb;
+    trtri_order(blockIdx.x, nt1, nt1, false, rb, cb);
+    if (cb < nt2) tile_at(rb, cb);
   }
 }
 
@@ -116,21 +154,21 @@ hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, cons
   if (!diag_done) trtri_diag_kernel<<<dim3(nblk, bt.count), WG, 0, c->stream>>>(Dinv, W, ldw, bt.dinv, bt.w);
   for (int h = 1; h < nblk; h *= 2) {
     const int groups = (nblk + 2 * h - 1) / (2 * h);
-    // 128x128 tiles (half the operand traffic per flop) once a level still fills the chip with them: >= 512 paired
-    // workgroups per problem (n = 16384: levels h >= 32; n = 8192: the last level; n <= 4096: never).  Decided per
+    // 128x128 tiles (half the operand traffic per flop) once a level still fills the chip with them: >= ~1024 tiles
+    // per problem (n = 16384: levels h >= 32; n = 8192: the last level; n <= 4096: never).  Decided per
     // problem size, not batch count, so a batched fit stays bit-identical to single fits.
     const int h128 = h / 2;
     if (h >= 2 && (int64_t)groups * h128 * ((h128 + 1) / 2) >= 512) {
-      trtri_t_kernel<128><<<dim3((h128 + 1) / 2, h128, groups * bt.count), WG, 0, c->stream>>>(
-          L, ldl, W, ldw, T, h, nblk, groups, bt.k, bt.w, bt.ws);
-      trtri_w_kernel<128><<<dim3(h128, (h128 + 1) / 2, groups * bt.count), WG, 0, c->stream>>>(W, ldw, T, h, nblk,
-                                                                                                groups, bt.w, bt.ws);
+      const dim3 grid(h128 * h128, 1, groups * bt.count);
+      trtri_t_kernel<128, false><<<grid, WG, 0, c->stream>>>(L, ldl, W, ldw, T, h, nblk, groups, bt.k, bt.w, bt.ws);
+      trtri_w_kernel<128, false><<<grid, WG, 0, c->stream>>>(W, ldw, T, h, nblk, groups, bt.w, bt.ws);
       continue;
     }
-    const int hp = (h + 1) / 2;  // paired tiles (load balance, see the kernels)
-    trtri_t_kernel<NB><<<dim3(hp, h, groups * bt.count), WG, 0, c->stream>>>(L, ldl, W, ldw, T, h, nblk, groups,
-                                                                             bt.k, bt.w, bt.ws);
-    trtri_w_kernel<NB><<<dim3(h, hp, groups * bt.count), WG, 0, c->stream>>>(W, ldw, T, h, nblk, groups, bt.w, bt.ws);
+    const int hp = (h + 1) / 2;  // paired tiles
+    trtri_t_kernel<NB, true><<<dim3(hp, h, groups * bt.count), WG, 0, c->stream>>>(L, ldl, W, ldw, T, h, nblk, groups,
+                                                                                   bt.k, bt.w, bt.ws);
+    trtri_w_kernel<NB, true><<<dim3(h, hp, groups * bt.count), WG, 0, c->stream>>>(W, ldw, T, h, nblk, groups, bt.w,
+                                                                                   bt.ws);
   }
   return hipGetLastError();
 }
