@@ -592,53 +592,65 @@ __device__ __forceinline__ void trail_tile(int t, int T, int M, int xmap, int& I
   I = J = 0;  // not reached: p < T
 }
 
-// The 128x128 tile with origin at 64-block (r0, q0): A -= sum_{k = k0}^{c-1} L_{r0..,k} L_{q0..,k}^T.
+// The 128 x TN tile with origin at 64-block (r0, q0): A -= sum_{k = k0}^{c-1} L_{r0..,k} L_{q0..,k}^T (TN = 128, or 64 for
+// the half tiles that end a long flush, StepPlan::nsplit; per element the same MFMA k order, so the same bits).
+template <int TN>
 __device__ __forceinline__ void trailing_tile_at(double* __restrict__ A, int64_t lda, int c, int k0, int cfirst, int r0,
                                                  int q0, double* lds) {
   const double* Li = A + (int64_t)r0 * NB * lda + (int64_t)k0 * NB;
   const double* Lj = A + (int64_t)q0 * NB * lda + (int64_t)k0 * NB;
   double* C = A + (int64_t)r0 * NB * lda + (int64_t)q0 * NB;
-  Tile128 tl;
+  using TileT = MfmaTile<2 * NB, TN, 16, false, false>;
+  TileT tl;
   // C - acc, stored for the 64-blocks (rb, cb) with cb >= c+1 and rb >= cb, one row group i at a time: row group 0's C
   // loads are issued before the last k-tile's MFMAs and group i+1's before group i's stores, so one load round trip is
   // exposed instead of one per group (seeding acc with -C before the product, as the 64x64 panel updates do, pushes this
   // 128x128 tile into 30 VGPR spills)
-  double cv[Tile128::WN][4];
+  double cv[TileT::WN][4];
   auto load_group = [&](int i) {
 #pragma unroll
-    for (int j = 0; j < Tile128::WN; ++j)
+    for (int j = 0; j < TileT::WN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) cv[j][r] = C[(int64_t)Tile128::row_of(i, r) * lda + Tile128::col_of(j)];
+      for (int r = 0; r < 4; ++r) cv[j][r] = C[(int64_t)TileT::row_of(i, r) * lda + TileT::col_of(j)];
   };
   tl.zero();
   tl.run_acc_peeled(Li, lda, Lj, lda, 0, (c - k0) * NB, lds, [&] { load_group(0); });
   const rsrc_t rc = buf_rsrc(C);
 #pragma unroll
-  for (int i = 0; i < Tile128::WM; ++i) {
+  for (int i = 0; i < TileT::WM; ++i) {
 #pragma unroll
-    for (int j = 0; j < Tile128::WN; ++j)
+    for (int j = 0; j < TileT::WN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) tl.acc[i][j][r] = cv[j][r] - tl.acc[i][j][r];
-    if (i + 1 < Tile128::WM) load_group(i + 1);
+    if (i + 1 < TileT::WM) load_group(i + 1);
     // write-through 16-byte pairs; a 16-column pair never straddles a 64-block, and rows r = 0, 1 (even lanes) or 2, 3
     // (odd lanes) of one lane lie in one 64-row block
 #pragma unroll
-    for (int j = 0; j < Tile128::WN; ++j) {
-      const int cb = q0 + (Tile128::col_of(j) >> 6);
+    for (int j = 0; j < TileT::WN; ++j) {
+      const int cb = q0 + (TileT::col_of(j) >> 6);
       const bool colok = cb >= cfirst;
-      const bool k01 = colok && r0 + (Tile128::row_of(i, 0) >> 6) >= cb;
-      const bool k23 = colok && r0 + (Tile128::row_of(i, 2) >> 6) >= cb;
-      store_block_pairs_sc1<Tile128>(rc, lda, i, j, tl.acc[i][j], k01, k23);
+      const bool k01 = colok && r0 + (TileT::row_of(i, 0) >> 6) >= cb;
+      const bool k23 = colok && r0 + (TileT::row_of(i, 2) >> 6) >= cb;
+      store_block_pairs_sc1<TileT>(rc, lda, i, j, tl.acc[i][j], k01, k23);
     }
   }
 }
 
+// Trailing workgroup p of a launch: tiles 0 .. ntile - nsplit - 1 whole, the last nsplit tiles as two 128 x 64 halves
+// (workgroups ntile - nsplit + 2h + half).
 __device__ __forceinline__ void trailing_role(double* __restrict__ A, int64_t lda, int c, int nblk, int k0, int cfirst,
-                                              int tile, int ntile, int xmap, double* lds) {
+                                              int p, int ntile, int nsplit, int xmap, double* lds) {
   const int M = (nblk - cfirst + 1) / 2, c0 = nblk - 2 * M;
+  const int nwhole = ntile - nsplit;
   int I, J;
-  trail_tile(tile, ntile, M, xmap, I, J);
-  trailing_tile_at(A, lda, c, k0, cfirst, c0 + 2 * I, c0 + 2 * J, lds);
+  if (p < nwhole) {
+    trail_tile(p, ntile, M, xmap, I, J);
+    trailing_tile_at<2 * NB>(A, lda, c, k0, cfirst, c0 + 2 * I, c0 + 2 * J, lds);
+  } else {
+    const int h = p - nwhole;
+    trail_tile(nwhole + (h >> 1), ntile, M, xmap, I, J);
+    trailing_tile_at<NB>(A, lda, c, k0, cfirst, c0 + 2 * I, c0 + 2 * J + (h & 1), lds);
+  }
 }
 
 // Lookahead workgroup (mode 1) of launch c: tile (c+1+idx, c+1) of the next panel's column gets every pending
@@ -672,6 +684,7 @@ struct StepPlan {
   int tbase, xmap;  // first trailing workgroup (a multiple of 8 when xmap: XCD-chunked tile order), tile order
   int split;        // panel row blocks c+1.. split into 1, 2 or 4 workgroups (panel workgroup b > 0: p = 1 + (b-1) / split)
   int overlap;      // the panels' first pivot block factored under their pre-update (update_eager OV)
+  int nsplit;       // the last nsplit trailing tiles run as two 128 x 64 halves each (ntrail + nsplit trailing workgroups)
 };
 
 // slots > 0: the co-resident workgroup slots a problem may fill (two per CU, shared by a batch); the panel row blocks are
@@ -713,6 +726,13 @@ inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush,
   // the overlapped pre-update shortens the panel chain but slows launches whose trailing workgroups do not all fit
   // the co-resident slots at once
   s.overlap = slots > 0 && s.tbase + s.ntrail <= slots;
+  // A long flush (K >= 256) of T tiles over S slots ends with a partial round of T mod S tiles; when that remainder fills
+  // at most half the slots, its tiles run as 128 x 64 halves, so the last round takes about half a tile time
+  s.nsplit = 0;
+  if (slots > 0 && flush && c - last_flush >= 4) {
+    const int r = s.ntrail % slots;
+    if (r > 0 && 2 * r <= slots) s.nsplit = r;
+  }
   return s;
 }
 
@@ -744,7 +764,7 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, StepPlan
   } else if (role == 1)
     lookahead_role(A, lda, c, s.look_a, b - s.npanel, lds);
   else
-    trailing_role(A, lda, c, nblk, s.k0, s.cfirst, b - s.tbase, s.ntrail, s.xmap, lds);
+    trailing_role(A, lda, c, nblk, s.k0, s.cfirst, b - s.tbase, s.ntrail, s.nsplit, s.xmap, lds);
   GPX_STEP_STAMP(role, c, b, 1);
 }
 
@@ -835,7 +855,7 @@ static void launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double*
   const int mode = potrf_mode(ctx, nblk);
   for_each_step(ctx, nblk, mode, cend, potrf_slots(ctx, bt.count), [&](int c, const StepPlan& s) {
     if (c < cbeg) return;
-    const dim3 grid(s.tbase + s.ntrail, bt.count);
+    const dim3 grid(s.tbase + s.ntrail + s.nsplit, bt.count);
     if (!f.r)
       potrf_step_kernel<0><<<grid, WG, 0, ctx->stream>>>(A, lda, c, nblk, s, Dinv, info, 0, bt.k, bt.dinv, f);
     else if (f.nrhs == 1)

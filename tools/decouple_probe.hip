@@ -78,7 +78,7 @@ __device__ __forceinline__ void near_role(double* __restrict__ A, int64_t lda, i
     __syncthreads();
     if (!s_ok) return;
   }
-  trailing_tile_at(A, lda, c, s.k0, s.cfirst, r0, q0, lds);
+  trailing_tile_at<2 * NB>(A, lda, c, s.k0, s.cfirst, r0, q0, lds);
 }
 
 // The far tiles (q0 >= D + 1, in q0 order, dealt round-robin to the workgroups; one workgroup per CU): pass after pass,
@@ -117,7 +117,7 @@ potrf_side_kernel(double* __restrict__ A, int64_t lda, int nblk, int D, int32_t*
       double* At = A;
       int64_t ldt = lda;
       asm volatile("" : "+s"(At), "+s"(ldt));
-      trailing_tile_at(At, ldt, ke, kb, 0, r0, q0, lds);
+      trailing_tile_at<2 * NB>(At, ldt, ke, kb, 0, r0, q0, lds);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (threadIdx.x == 0)
@@ -138,9 +138,9 @@ dec_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, DPlan d, d
   const int b = (int)blockIdx.x;
   if (b < s.npanel) {
     if (s.split == 2 && b > 0)
-      panel_role<0, 2>(A, lda, c, 1 + ((b - 1) >> 1), (b - 1) & 1, nblk, s.c0, Dinv, info, lds, PotrfFwd());
+      panel_role<0, 2>(A, lda, c, 1 + ((b - 1) >> 1), (b - 1) & 1, nblk, s.c0, Dinv, info, lds, PotrfFwd(), s.overlap);
     else
-      panel_role<0, 1>(A, lda, c, b, 0, nblk, s.c0, Dinv, info, lds, PotrfFwd());
+      panel_role<0, 1>(A, lda, c, b, 0, nblk, s.c0, Dinv, info, lds, PotrfFwd(), s.overlap);
     if (b > 0) {  // L_ic stored write-through: drain, barrier, publish the rows
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -184,9 +184,9 @@ near_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, StepPlan 
   const int b = (int)blockIdx.x;
   if (b < s.npanel) {
     if (s.split == 2 && b > 0)
-      panel_role<0, 2>(A, lda, c, 1 + ((b - 1) >> 1), (b - 1) & 1, nblk, s.c0, Dinv, info, lds, PotrfFwd());
+      panel_role<0, 2>(A, lda, c, 1 + ((b - 1) >> 1), (b - 1) & 1, nblk, s.c0, Dinv, info, lds, PotrfFwd(), s.overlap);
     else
-      panel_role<0, 1>(A, lda, c, b, 0, nblk, s.c0, Dinv, info, lds, PotrfFwd());
+      panel_role<0, 1>(A, lda, c, b, 0, nblk, s.c0, Dinv, info, lds, PotrfFwd(), s.overlap);
     return;
   }
   if (b < s.tbase) return;
@@ -195,7 +195,7 @@ near_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, StepPlan 
   for (int J = 0; J < M; ++J) {
     if (c0 + 2 * J - c >= D) return;
     if (p < M - J) {
-      trailing_tile_at(A, lda, c, s.k0, s.cfirst, c0 + 2 * (J + p), c0 + 2 * J, lds);
+      trailing_tile_at<2 * NB>(A, lda, c, s.k0, s.cfirst, c0 + 2 * (J + p), c0 + 2 * J, lds);
       return;
     }
     p -= M - J;
