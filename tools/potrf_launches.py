@@ -10,7 +10,7 @@ if not path.endswith(".csv"):
     path = sorted(glob.glob(path + "/**/*kernel_trace.csv", recursive=True))[-1]
 rows = list(csv.DictReader(open(path)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if "gram_kernel" in r["Kernel_Name"]][-1]
+idx = [i for i, r in enumerate(rows) if "gram" in r["Kernel_Name"]][-1]
 seq = [r for r in rows[idx:] if "potrf_step" in r["Kernel_Name"]]
 durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in seq]
 print(f"{len(durs)} launches: sum {sum(durs):.1f} us")
