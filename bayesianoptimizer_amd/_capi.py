@@ -59,7 +59,7 @@ class NotPositiveDefiniteError(GPXError):
 
 
 class GPXTimeoutError(GPXError):
-    """A persistent launch (the dataflow Cholesky or the triangular solve) gave up on an in-launch hand-off after its
+    """A persistent launch (the triangular solve) gave up on an in-launch hand-off after its
     bounded spin: the factor / alpha of that call are invalid.  Distinct from NotPositiveDefiniteError, because a larger
     jitter (the reference's retry, optimization/Bayesian6.py:481-488) does not cure it."""
 

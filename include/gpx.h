@@ -133,7 +133,7 @@ size_t gpx_acq_params_size(void);
 /* Per-handle options (tuning and diagnostics; every default is the measured best).  gpx_create reads the environment
  * variable GPX_OPTIONS once ("name=value,name=value", names as below in lower case without the prefix, e.g.
  * "sweep_fused=0,potrf_mode=1"); nothing else in the library reads the environment.
- *  GPX_OPT_SPIN_LIMIT      polls before an in-launch hand-off (Cholesky dataflow, triangular solve) gives up and
+ *  GPX_OPT_SPIN_LIMIT      polls before an in-launch hand-off (the triangular solve's) gives up and
  *                          reports GPX_INFO_TIMEOUT (default 4194304; 0 = give up at the first unmet poll: tests)
  *  GPX_OPT_SWEEP_FUSED     1 (default) the fused small-n sweep where it applies (padded n <= 256), 0 the K* + trmm path
  *  GPX_OPT_GRAM_SPLIT      0 by size (default), else 1, 2 or 4 workgroups per 64x64 Gram tile
