@@ -14,11 +14,16 @@ using namespace gpx;
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 constexpr int TT = 128;
 
-template <int BK>
+template <int BK, int STAGGER = 0>
 __device__ __forceinline__ void trmm_body(const double* __restrict__ W, int64_t ldw, const double* __restrict__ kstar,
                                           int64_t C, int nI, int ncb, double* __restrict__ ss_part, double* smem) {
   using Tile = MfmaTile<TT, TT, BK, true, true>;
   const int b = blockIdx.x;
+  // STAGGER > 0: workgroups with bit STAGGER of b set start ~half a k-tile later (two co-resident workgroups out of step)
+  if constexpr (STAGGER > 0) {
+    if ((b >> STAGGER) & 1)
+      __builtin_amdgcn_s_sleep(64);  // ~4096 cycles
+  }
   const int x = b & 7, l = b >> 3, per = ncb >> 3;
   const int I = nI - 1 - l / per, cb = 8 * (l % per) + x;
   Tile tile;
@@ -53,6 +58,12 @@ __global__ void __launch_bounds__(256) trmm_bk16(const double* W, int64_t ldw, c
   __shared__ __attribute__((aligned(16))) double smem[MfmaTile<TT, TT, 16, true, true>::LDS_DOUBLES];
   trmm_body<16>(W, ldw, K, C, nI, ncb, ss, smem);
 }
+template <int ST>
+__global__ void __launch_bounds__(256) trmm_stagger(const double* W, int64_t ldw, const double* K, int64_t C, int nI,
+                                                    int ncb, double* ss) {
+  __shared__ __attribute__((aligned(16))) double smem[MfmaTile<TT, TT, 16, true, true>::LDS_DOUBLES];
+  trmm_body<16, ST>(W, ldw, K, C, nI, ncb, ss, smem);
+}
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 trmm_bk32(const double* W, int64_t ldw, const double* K, int64_t C, int nI, int ncb, double* ss) {
   extern __shared__ __attribute__((aligned(16))) double dsmem[];
@@ -84,12 +95,17 @@ int main() {
   const size_t lds32 = MfmaTile<TT, TT, 32, true, true>::LDS_DOUBLES * 8, lds_occ1 = 100 * 1024;
   CK(hipFuncSetAttribute((const void*)trmm_bk32, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds32));
   CK(hipFuncSetAttribute((const void*)trmm_bk16_occ1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_occ1));
-  const char* names[] = {"BK16 2 WG/CU (shipped)", "BK32 1 WG/CU", "BK16 1 WG/CU"};
+  const char* names[] = {"BK16 2 WG/CU (shipped)", "BK32 1 WG/CU", "BK16 1 WG/CU", "stagger bit 8", "stagger bit 3",
+                         "stagger bit 5"};
+  constexpr int NV = 6;
   auto run = [&](int v, double* out) {
     const dim3 g(ncb * nI);
     if (v == 0) trmm_bk16<<<g, 256>>>(W, n, K, C, nI, ncb, out);
     else if (v == 1) trmm_bk32<<<g, 256, lds32>>>(W, n, K, C, nI, ncb, out);
-    else trmm_bk16_occ1<<<g, 256, lds_occ1>>>(W, n, K, C, nI, ncb, out);
+    else if (v == 2) trmm_bk16_occ1<<<g, 256, lds_occ1>>>(W, n, K, C, nI, ncb, out);
+    else if (v == 3) trmm_stagger<8><<<g, 256>>>(W, n, K, C, nI, ncb, out);
+    else if (v == 4) trmm_stagger<3><<<g, 256>>>(W, n, K, C, nI, ncb, out);
+    else trmm_stagger<5><<<g, 256>>>(W, n, K, C, nI, ncb, out);
   };
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -99,7 +115,7 @@ int main() {
   CK(hipGetLastError());
   std::vector<double> ref((size_t)nI * C), got((size_t)nI * C);
   CK(hipMemcpy(ref.data(), ss0, ref.size() * 8, hipMemcpyDeviceToHost));
-  for (int v = 1; v < 3; ++v) {
+  for (int v = 1; v < NV; ++v) {
     CK(hipMemset(ss1, 0, (size_t)nI * C * 8));
     run(v, ss1);
     CK(hipDeviceSynchronize());
@@ -110,9 +126,9 @@ int main() {
     printf("%-24s bitwise mismatches vs shipped: %zu\n", names[v], bad);
   }
   const double flops = (double)n * n * C;
-  std::vector<std::vector<float>> t(3);
+  std::vector<std::vector<float>> t(NV);
   for (int rep = 0; rep < 8; ++rep)
-    for (int v = 0; v < 3; ++v) {
+    for (int v = 0; v < NV; ++v) {
       CK(hipEventRecord(e0));
       run(v, ss1);
       CK(hipEventRecord(e1));
@@ -121,7 +137,7 @@ int main() {
       CK(hipEventElapsedTime(&ms, e0, e1));
       t[v].push_back(ms);
     }
-  for (int v = 0; v < 3; ++v) {
+  for (int v = 0; v < NV; ++v) {
     std::sort(t[v].begin(), t[v].end());
     const float med = t[v][t[v].size() / 2];
     printf("%-24s median %.3f ms min %.3f ms -> %.2f TF/s (frac %.4f)\n", names[v], med, t[v][0],
