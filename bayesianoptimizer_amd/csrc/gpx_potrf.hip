@@ -732,6 +732,11 @@ inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush,
   if (slots > 0 && flush && c - last_flush >= 4) {
     const int r = s.ntrail % slots;
     if (r > 0 && 2 * r <= slots) s.nsplit = r;
+  } else if (slots > 0 && flush) {
+    // an eager launch (K = 64) that overflows the co-resident slots by a few tiles (n = 4096, c = 1..4: 63 panels +
+    // 496 tiles over 512 slots) would run them as a second round of whole tiles: halves instead
+    const int over = s.tbase + s.ntrail - slots;
+    if (over > 0 && 4 * over <= slots) s.nsplit = over < s.ntrail ? over : s.ntrail;
   }
   return s;
 }
