@@ -12,12 +12,15 @@
 //        U  A_ij -= L_is L_js^T for the trailing 16x16 blocks of the panel (fp64 MFMA),
 //    with a one-block lookahead: wave 0 does the T and U of the next pivot block itself and goes straight on to the
 //    next F (one barrier per step); waves 1-3 do the other T items, wait on an LDS counter until every T item of the
-//    step is published, and do the other U items while that F runs.  Every panel workgroup re-factors A_cc (no
+//    step is published, and do the other U items while that F runs.  Where a launch's workgroups all fit the
+//    co-resident slots, the first F runs on wave 0 under the other waves' pre-update MFMAs (update_eager OV).
+//    Every panel workgroup re-factors A_cc (no
 //    extra latency, no extra launch); p = 0 stores L_cc in the scratch half of Dinv (A_cc must stay intact while
 //    the other panel workgroups read it), p > 0 store L_ic.
 //  * trailing workgroups apply the step-(c-1) update to every lower tile of columns >= c+1:
 //    A_ij -= L_{i,c-1} L_{j,c-1}^T on 128x128 MfmaTiles (half the HBM/L2 traffic per flop of 64x64 tiles; the
-//    update is traffic-bound at 64x64: 36 us for the 2016 tiles of step 0).
+//    update is traffic-bound at 64x64: 36 us for the 2016 tiles of step 0); tiles that would run as a last, partly
+//    empty round of slots run as 128x64 halves instead (StepPlan::nsplit).
 // Column c+1 is thus updated by step c-1 in launch c and by step c inside the panel workgroups of launch c+1, so
 // the panel factorisation (the latency-bound serial chain) overlaps the trailing update of the previous step
 // instead of following it.  For large n the trailing update is flushed lazily (every g block columns, K = 64 g:
@@ -80,9 +83,10 @@ __device__ __forceinline__ void update_to_lds(Tile64& tl, const double* __restri
 // all 16, into sA / sP.  Every global load of the step - L_c, L_i and the C seeds of the wave's blocks - is issued in one
 // straight-line burst (MfmaTile's 16-k pipeline exposed a global round trip per k-tile: ~7 us for the two products
 // against ~3 us of MFMA); the seeds are +C and the products subtract through the MFMA's A-operand negation (neg:[1,0,0]),
-// so nothing waits on a seed before the first MFMA needs it.  Wave W owns A_ic's block row W and the A_cc blocks
-// W, W+4, W+8 of the row-major lower list, each a K = 64 chain of 16 MFMAs in MfmaTile's k order (C - ab rounds as
-// -(-C + ab): same results).  sA / sP double as the staging: the products are held in registers across a barrier.
+// so nothing waits on a seed before the first MFMA needs it.  Each wave owns the blocks of its lists (kPreCC / kPreIC
+// below: indices into the row-major lower list kLowerBlk and A_ic blocks), each a K = 64 chain of 16 MFMAs in MfmaTile's
+// k order (C - ab rounds as -(-C + ab): same results).  sA / sP double as the staging: the products are held in
+// registers across a barrier.
 constexpr int kLowerBlk[10][2] = {{0, 0}, {1, 0}, {1, 1}, {2, 0}, {2, 1}, {2, 2}, {3, 0}, {3, 1}, {3, 2}, {3, 3}};
 
 __device__ __forceinline__ d4 mfma_sub(double a, double b, d4 c) {  // c - a b
