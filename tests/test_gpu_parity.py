@@ -161,10 +161,13 @@ def test_alpha(engine, nrhs):
 
 
 @pytest.mark.parametrize("n,nrhs,kind", [(1, 1, "rbf"), (128, 2, "matern52"), (333, 1, "rbf"), (1100, 8, "rbf"),
-                                         (2500, 3, "scale_linear_matern52"), (4096, 1, "rbf")])
+                                         (2500, 3, "scale_linear_matern52"), (4096, 1, "rbf"), (4100, 2, "matern52"),
+                                         (6000, 1, "rbf")])
 def test_potrs_alpha_matches_inverse_path_and_oracle(engine, n, nrhs, kind):
     """alpha by the triangular solves on L (gpx_fit_factor_f64 / gpx_potrs_f64, no W) against alpha = W W^T (y - m) of
-    the inverse path (gpx_fit_f64) and the oracle; the factor-only state builds the same W on first use."""
+    the inverse path (gpx_fit_f64) and the oracle; the factor-only state builds the same W on first use.  n = 4096: the
+    eager schedule with the overlapped first pivot block and the overflow half tiles of launches 1-4; n = 4100 / 6000
+    (padded 4224 / 6016): the lookahead schedule with lazy flushes ending in half tiles."""
     d = 5
     X, y = O.synthetic_problem(n, d, 40 + n)
     Y = np.stack([y * (r + 1) - 0.3 * r for r in range(nrhs)], 1)
