@@ -820,14 +820,17 @@ __global__ void __launch_bounds__(WG) potrf_dinv_kernel(double* __restrict__ A, 
 // to their own tiles.  Schedule by size (tools/lazy_sweep.sh, profiles/r01_potrf_lazy_sweep*.log):
 //   n = 4096:  mode 0, g = 1 -> potrf 1.73-1.75 ms (mode 1 g = 2/4: 1.81/1.94: a K = 128 flush tile is >= 14 us of
 //              MFMA on one CU, longer than the ~20 us panel window once two share a CU);
-//   n = 8192:  mode 1, g = 4 -> 6.34 ms (mode 0 g = 2: 6.69);
+//   n = 8192:  mode 1, g = 4 -> 6.34 ms (mode 0 g = 2: 6.69); round 4, with the half-tile flush tails: g = 6 5.83 ms
+//              against g = 4 / 7 / 8: 5.90 / 5.96 / 5.95 (profiles/r04_lazy_interval_ab.log), while n = 6000 (94 blocks)
+//              keeps g = 4 (3.165 vs 3.179 / 3.183 ms for g = 5 / 6) and n = 16384 g = 8 (30.16 vs 30.60 / 30.31 for
+//              g = 6 / 10);
 //   n = 16384: mode 1, g = 8 -> 31.4 ms (mode 0 g = 4: 34.4, g = 1: 46.3).
 // The handle options GPX_OPT_POTRF_LAZY / GPX_OPT_POTRF_MODE override.  Flushing every second launch only in the early,
 // trailing-bound launches and panel-wave priority were measured neutral (DESIGN.md §5, items 14 and the prio knob)
 // and are not offered.  Trailing tiles are dealt to the XCDs in 8 x 8 super-block chunks (trail_tile xmap = 1).
 static int potrf_lazy(const Context* ctx, int nblk) {
   if (ctx->potrf_lazy > 0) return ctx->potrf_lazy;
-  return nblk > 128 ? 8 : (nblk > 64 ? 4 : 1);
+  return nblk > 128 ? 8 : (nblk > 100 ? 6 : (nblk > 64 ? 4 : 1));
 }
 
 static int potrf_mode(const Context* ctx, int nblk) {
