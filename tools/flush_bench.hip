@@ -15,11 +15,17 @@
 using namespace gpx;
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
-template <bool KM>
+template <bool KM, int STAG = 0, int EPI = 0>
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
 flush_kernel(double* __restrict__ Cm, int64_t ldc, const double* __restrict__ L, int64_t ldl, int K) {
   using T = MfmaTile<128, 128, 16, KM, KM>;
   __shared__ __attribute__((aligned(16))) double lds[T::LDS_DOUBLES];
+  // STAG > 0: the odd workgroups of the first round start STAG x ~3.4 us late, so the rounds after it are out of step
+  // (every tile has the same K: the grid otherwise runs in lockstep rounds whose C loads / stores all fall together)
+  if constexpr (STAG > 0) {
+    if (blockIdx.x < 512 && (blockIdx.x & 1))
+      for (int i = 0; i < STAG; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   int I, J;
   tri_decode((int)blockIdx.x, I, J);
   // row-major: L[i][k] (ldl = K); k-major: LT[k][i] (ldl = m)
@@ -35,8 +41,89 @@ flush_kernel(double* __restrict__ Cm, int64_t ldc, const double* __restrict__ L,
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         double* p = C + (int64_t)T::row_of(i, r) * ldc + T::col_of(j);
-        *p = *p - tl.acc[i][j][r];
+        if constexpr (EPI == 0) *p = *p - tl.acc[i][j][r];  // read-modify-write C (the flush)
+        if constexpr (EPI == 1) *p = tl.acc[i][j][r];       // store only (timing: no C read)
+        if constexpr (EPI == 2)                              // nothing stored unless impossible (timing: no C traffic)
+          if (tl.acc[i][j][r] == 12345.678) *p = 0.0;
       }
+}
+
+// F5: persistent workgroups (one per slot) walking tiles b, b + grid, ...: the last k-tile of a tile issues the next
+// tile's first k-tile loads and this tile's first C row group, and stores the next tile's k-tile into the idle LDS
+// buffer, so the next tile starts without a load round trip and the C epilogue runs while those loads are in flight.
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
+flush_persistent(double* __restrict__ Cm, int64_t ldc, const double* __restrict__ L, int64_t ldl, int K, int tiles) {
+  using T = MfmaTile<128, 128, 16, false, false>;
+  constexpr int BK = 16;
+  __shared__ __attribute__((aligned(16))) double lds[T::LDS_DOUBLES];
+  double* cur = lds;
+  double* nxt = lds + BK * (T::PA + T::PB);
+  int t = (int)blockIdx.x;
+  if (t >= tiles) return;
+  int I, J;
+  tri_decode(t, I, J);
+  const double* A = L + (int64_t)I * 128 * ldl;
+  const double* B = L + (int64_t)J * 128 * ldl;
+  T tl;
+  tl.load_regs(A, ldl, B, ldl, 0);
+  tl.store_lds(cur, cur + BK * T::PA);
+  __syncthreads();
+#pragma unroll 1
+  while (true) {
+    const int tn = t + (int)gridDim.x;
+    const bool has_next = tn < tiles;
+    int In = 0, Jn = 0;
+    if (has_next) tri_decode(tn, In, Jn);
+    const double* An = L + (int64_t)In * 128 * ldl;
+    const double* Bn = L + (int64_t)Jn * 128 * ldl;
+    double* C = Cm + (int64_t)I * 128 * ldc + (int64_t)J * 128;
+    tl.zero();
+#pragma unroll 1
+    for (int k0 = 0; k0 + BK < K; k0 += BK) {
+      tl.load_regs(A, ldl, B, ldl, k0 + BK);
+      tl.compute(cur, cur + BK * T::PA);
+      tl.store_lds(nxt, nxt + BK * T::PA);
+      __syncthreads();
+      double* x = cur;
+      cur = nxt;
+      nxt = x;
+    }
+    if (has_next) tl.load_regs(An, ldl, Bn, ldl, 0);
+    double cv[T::WN][4];
+    auto load_group = [&](int i) {
+#pragma unroll
+      for (int j = 0; j < T::WN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cv[j][r] = C[(int64_t)T::row_of(i, r) * ldc + T::col_of(j)];
+    };
+    load_group(0);
+    tl.compute(cur, cur + BK * T::PA);
+    if (has_next) tl.store_lds(nxt, nxt + BK * T::PA);
+    __syncthreads();
+    {
+      double* x = cur;
+      cur = nxt;
+      nxt = x;
+    }
+#pragma unroll
+    for (int i = 0; i < T::WM; ++i) {
+#pragma unroll
+      for (int j = 0; j < T::WN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tl.acc[i][j][r] = cv[j][r] - tl.acc[i][j][r];
+      if (i + 1 < T::WM) load_group(i + 1);
+#pragma unroll
+      for (int j = 0; j < T::WN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) C[(int64_t)T::row_of(i, r) * ldc + T::col_of(j)] = tl.acc[i][j][r];
+    }
+    if (!has_next) break;
+    t = tn;
+    I = In;
+    J = Jn;
+    A = An;
+    B = Bn;
+  }
 }
 
 int main(int argc, char** argv) {
@@ -70,22 +157,58 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const double flops = 2.0 * 128 * 128 * (double)K * tiles;
-  std::vector<float> t[2];
+  constexpr int NV = 8;
+  int dev = 0, cus = 0;
+  CK(hipGetDevice(&dev));
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  {  // F5 against F0, bit for bit (same MFMA order per tile)
+    double* C2;
+    CK(hipMalloc(&C2, (size_t)m * m * 8));
+    CK(hipMemset(C2, 0, (size_t)m * m * 8));
+    CK(hipMemset(C0, 0, (size_t)m * m * 8));
+    flush_kernel<false><<<tiles, WG>>>(C0, m, L, K, K);
+    flush_persistent<<<std::min(tiles, 2 * cus), WG>>>(C2, m, L, K, K, tiles);
+    CK(hipDeviceSynchronize());
+    CK(hipGetLastError());
+    std::vector<double> a((size_t)m * m), b((size_t)m * m);
+    CK(hipMemcpy(a.data(), C0, a.size() * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), C2, b.size() * 8, hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (size_t q = 0; q < a.size(); ++q) bad += a[q] != b[q];
+    printf("F5 vs F0 bitwise mismatches %zu\n", bad);
+    CK(hipFree(C2));
+  }
+  std::vector<float> t[NV];
   for (int rep = 0; rep < 10; ++rep)
-    for (int v = 0; v < 2; ++v) {
+    for (int v = 0; v < NV; ++v) {
       CK(hipEventRecord(e0));
       if (v == 0)
         flush_kernel<false><<<tiles, WG>>>(C0, m, L, K, K);
-      else
+      else if (v == 1)
         flush_kernel<true><<<tiles, WG>>>(C1, m, LT, m, K);
+      else if (v == 2)
+        flush_kernel<false, 4><<<tiles, WG>>>(C0, m, L, K, K);
+      else if (v == 3)
+        flush_kernel<false, 8><<<tiles, WG>>>(C0, m, L, K, K);
+      else if (v == 4)
+        flush_kernel<false, 16><<<tiles, WG>>>(C0, m, L, K, K);
+      else if (v == 5)
+        flush_persistent<<<std::min(tiles, 2 * cus), WG>>>(C0, m, L, K, K, tiles);
+      else if (v == 6)
+        flush_kernel<false, 0, 1><<<tiles, WG>>>(C1, m, L, K, K);
+      else
+        flush_kernel<false, 0, 2><<<tiles, WG>>>(C1, m, L, K, K);
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
       t[v].push_back(ms);
     }
-  const char* names[2] = {"F0 row-major (swizzled LDS transpose)", "F1 k-major (16-byte LDS writes)"};
-  for (int v = 0; v < 2; ++v) {
+  const char* names[NV] = {"F0 row-major (swizzled LDS transpose)", "F1 k-major (16-byte LDS writes)",
+                           "F0, first round staggered ~14 us", "F0, first round staggered ~27 us",
+                           "F0, first round staggered ~55 us", "F5 persistent, next tile prefetched",
+                           "F0 timing: C stored, not read", "F0 timing: no C traffic"};
+  for (int v = 0; v < NV; ++v) {
     std::sort(t[v].begin(), t[v].end());
     const float med = t[v][t[v].size() / 2];
     printf("%-40s median %.3f ms -> %.1f TF/s\n", names[v], med, flops / (med * 1e-3) / 1e12);
