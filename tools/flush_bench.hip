@@ -126,6 +126,72 @@ flush_persistent(double* __restrict__ Cm, int64_t ldc, const double* __restrict_
   }
 }
 
+// F7 / F8: the library's trailing tile (peeled last k-tile with C row group 0 loaded under it, group i+1 loaded before
+// group i's stores) with (PF) / without an L2 prefetch of the C tile a few k-tiles before the end: each thread touches
+// four of the tile's 128-byte lines with plain loads whose values feed an empty asm at the epilogue, so the loads stay
+// alive, retire under the k loop's MFMAs and leave the lines in L2 for the epilogue's reads.
+template <bool PF>
+__global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
+flush_lib(double* __restrict__ Cm, int64_t ldc, const double* __restrict__ L, int64_t ldl, int K) {
+  using T = MfmaTile<128, 128, 16, false, false>;
+  constexpr int BK = 16;
+  __shared__ __attribute__((aligned(16))) double lds[T::LDS_DOUBLES];
+  int I, J;
+  tri_decode((int)blockIdx.x, I, J);
+  const double* A = L + (int64_t)I * 128 * ldl;
+  const double* B = L + (int64_t)J * 128 * ldl;
+  double* C = Cm + (int64_t)I * 128 * ldc + (int64_t)J * 128;
+  T tl;
+  tl.zero();
+  double* cur = lds;
+  double* nxt = lds + BK * (T::PA + T::PB);
+  tl.load_regs(A, ldl, B, ldl, 0);
+  tl.store_lds(cur, cur + BK * T::PA);
+  __syncthreads();
+  double pf[4] = {0.0, 0.0, 0.0, 0.0};
+  const int t = threadIdx.x;
+  for (int k0 = 0; k0 + BK < K; k0 += BK) {
+    tl.load_regs(A, ldl, B, ldl, k0 + BK);
+    if constexpr (PF) {
+      if (k0 + 4 * BK == K) {  // three k-tiles before the end
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int line = t + q * WG;  // 1024 lines: row line / 8, 16 doubles each
+          pf[q] = C[(int64_t)(line >> 3) * ldc + (line & 7) * 16];
+        }
+      }
+    }
+    tl.compute(cur, cur + BK * T::PA);
+    tl.store_lds(nxt, nxt + BK * T::PA);
+    __syncthreads();
+    double* x = cur;
+    cur = nxt;
+    nxt = x;
+  }
+  double cv[T::WN][4];
+  auto load_group = [&](int i) {
+#pragma unroll
+    for (int j = 0; j < T::WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cv[j][r] = C[(int64_t)T::row_of(i, r) * ldc + T::col_of(j)];
+  };
+  load_group(0);
+  tl.compute(cur, cur + BK * T::PA);
+  if constexpr (PF) asm volatile("" ::"v"(pf[0]), "v"(pf[1]), "v"(pf[2]), "v"(pf[3]));
+#pragma unroll
+  for (int i = 0; i < T::WM; ++i) {
+#pragma unroll
+    for (int j = 0; j < T::WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tl.acc[i][j][r] = cv[j][r] - tl.acc[i][j][r];
+    if (i + 1 < T::WM) load_group(i + 1);
+#pragma unroll
+    for (int j = 0; j < T::WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) C[(int64_t)T::row_of(i, r) * ldc + T::col_of(j)] = tl.acc[i][j][r];
+  }
+}
+
 int main(int argc, char** argv) {
   const int m = argc > 1 ? atoi(argv[1]) : 15872, K = argc > 2 ? atoi(argv[2]) : 512;
   const int M = m / 128, tiles = M * (M + 1) / 2;
@@ -157,7 +223,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const double flops = 2.0 * 128 * 128 * (double)K * tiles;
-  constexpr int NV = 8;
+  constexpr int NV = 10;
   int dev = 0, cus = 0;
   CK(hipGetDevice(&dev));
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -176,6 +242,13 @@ int main(int argc, char** argv) {
     size_t bad = 0;
     for (size_t q = 0; q < a.size(); ++q) bad += a[q] != b[q];
     printf("F5 vs F0 bitwise mismatches %zu\n", bad);
+    CK(hipMemset(C2, 0, (size_t)m * m * 8));
+    flush_lib<true><<<tiles, WG>>>(C2, m, L, K, K);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(b.data(), C2, b.size() * 8, hipMemcpyDeviceToHost));
+    bad = 0;
+    for (size_t q = 0; q < a.size(); ++q) bad += a[q] != b[q];
+    printf("F7 vs F0 bitwise mismatches %zu\n", bad);
     CK(hipFree(C2));
   }
   std::vector<float> t[NV];
@@ -196,8 +269,12 @@ int main(int argc, char** argv) {
         flush_persistent<<<std::min(tiles, 2 * cus), WG>>>(C0, m, L, K, K, tiles);
       else if (v == 6)
         flush_kernel<false, 0, 1><<<tiles, WG>>>(C1, m, L, K, K);
-      else
+      else if (v == 7)
         flush_kernel<false, 0, 2><<<tiles, WG>>>(C1, m, L, K, K);
+      else if (v == 8)
+        flush_lib<false><<<tiles, WG>>>(C0, m, L, K, K);
+      else
+        flush_lib<true><<<tiles, WG>>>(C0, m, L, K, K);
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;
@@ -207,7 +284,8 @@ int main(int argc, char** argv) {
   const char* names[NV] = {"F0 row-major (swizzled LDS transpose)", "F1 k-major (16-byte LDS writes)",
                            "F0, first round staggered ~14 us", "F0, first round staggered ~27 us",
                            "F0, first round staggered ~55 us", "F5 persistent, next tile prefetched",
-                           "F0 timing: C stored, not read", "F0 timing: no C traffic"};
+                           "F0 timing: C stored, not read", "F0 timing: no C traffic",
+                           "F8 library epilogue", "F7 library epilogue + C prefetch"};
   for (int v = 0; v < NV; ++v) {
     std::sort(t[v].begin(), t[v].end());
     const float med = t[v][t[v].size() / 2];
