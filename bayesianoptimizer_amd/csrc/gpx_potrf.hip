@@ -668,7 +668,30 @@ __device__ __forceinline__ void lookahead_role(double* __restrict__ A, int64_t l
   double* C = A + (int64_t)i * NB * lda + (int64_t)j * NB;
   Tile64 tl;
   tl.load_neg_c(C, lda);
-  tl.run_acc(Li, lda, Lj, lda, 0, (c - a) * NB, lds);
+  // K = 64 (c - a) up to 64 g in k-tiles of 16 with LA = 4 k-tiles of loads in flight (register stages st[]): a k-tile's
+  // 16 MFMAs per wave (~0.4 us) cover far less than a load round trip, so MfmaTile's one-ahead prefetch left this
+  // (latency-bound, few workgroups) tile waiting on every k-tile.  One barrier per k-tile, LDS double-buffered.  Same
+  // MFMA order, same bits.  n = 16384 update 30.09 -> 29.95 ms, n = 8192 5.88 -> 5.84 (LA = 8: 30.15 / 5.87,
+  // profiles/r04_lookahead_prefetch_ab.log).
+  constexpr int LA = 4;
+  const int nk = (c - a) * (NB / 16);  // a multiple of 4
+  Tile64 st[LA];
+  double* buf0 = lds;
+  double* buf1 = lds + 16 * (Tile64::PA + Tile64::PB);
+#pragma unroll
+  for (int q = 0; q < LA; ++q) st[q].load_regs(Li, lda, Lj, lda, 16 * q);
+  for (int k0 = 0; k0 < nk; k0 += LA) {
+#pragma unroll
+    for (int q = 0; q < LA; ++q) {
+      const int kt = k0 + q;
+      double* cur = (q & 1) ? buf1 : buf0;
+      st[q].store_lds(cur, cur + 16 * Tile64::PA);
+      __syncthreads();
+      if (kt + LA < nk) st[q].load_regs(Li, lda, Lj, lda, 16 * (kt + LA));
+      tl.compute(cur, cur + 16 * Tile64::PA);
+    }
+  }
+  __syncthreads();  // the last k-tile's LDS reads before the workgroup's next use of lds
   const rsrc_t rc = buf_rsrc(C);
 #pragma unroll
   for (int ii = 0; ii < Tile64::WM; ++ii)
