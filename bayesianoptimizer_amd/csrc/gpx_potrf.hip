@@ -848,23 +848,28 @@ __global__ void __launch_bounds__(WG) potrf_dinv_kernel(double* __restrict__ A, 
 //              keeps g = 4 (3.165 vs 3.179 / 3.183 ms for g = 5 / 6) and n = 16384 g = 8 (30.16 vs 30.60 / 30.31 for
 //              g = 6 / 10);
 //   n = 16384: mode 1, g = 8 -> 31.4 ms (mode 0 g = 4: 34.4, g = 1: 46.3).
+// Batched fits share the co-resident slots, so the per-launch panel chain is hidden under more trailing work: at
+// n = 4096 (64 blocks) the lookahead schedule wins from two problems up (profiles/r04_batched_lazy_sweep.log, update ms
+// eager g = 1 -> mode 1 g = 4 / 6): B = 2 2.313 -> 2.186 / 2.207, B = 3 2.991 -> 2.784 / 2.792, B = 4 3.778 -> 3.326 /
+// 3.287, B = 8 6.92 -> 5.56 / 5.43; at n = 2048 the eager schedule stays best for B = 2 / 4 (B = 8: 1.314 vs 1.302).
 // The handle options GPX_OPT_POTRF_LAZY / GPX_OPT_POTRF_MODE override.  Flushing every second launch only in the early,
 // trailing-bound launches and panel-wave priority were measured neutral (DESIGN.md §5, items 14 and the prio knob)
 // and are not offered.  Trailing tiles are dealt to the XCDs in 8 x 8 super-block chunks (trail_tile xmap = 1).
-static int potrf_lazy(const Context* ctx, int nblk) {
+static int potrf_lazy(const Context* ctx, int nblk, int batch) {
   if (ctx->potrf_lazy > 0) return ctx->potrf_lazy;
+  if (nblk == 64 && batch >= 2) return batch >= 4 ? 6 : 4;
   return nblk > 128 ? 8 : (nblk > 100 ? 6 : (nblk > 64 ? 4 : 1));
 }
 
-static int potrf_mode(const Context* ctx, int nblk) {
+static int potrf_mode(const Context* ctx, int nblk, int batch) {
   if (ctx->potrf_mode == 0 || ctx->potrf_mode == 1) return ctx->potrf_mode;
-  return nblk > 64 ? 1 : 0;
+  return nblk > 64 || (nblk == 64 && batch >= 2) ? 1 : 0;
 }
 
 // The plan of every launch c < cend (flush launches: c >= 1 and at least one interval after the previous flush).
 template <typename F>
-static void for_each_step(const Context* ctx, int nblk, int mode, int cend, int slots, F&& f) {
-  const int g = potrf_lazy(ctx, nblk);
+static void for_each_step(const Context* ctx, int nblk, int batch, int mode, int cend, int slots, F&& f) {
+  const int g = potrf_lazy(ctx, nblk, batch);
   int last = 0;
   for (int c = 0; c < cend; ++c) {
     const bool flush = c >= 1 && c - last >= g;
@@ -887,8 +892,8 @@ static int potrf_slots(Context* ctx, int batch) {
 
 static void launch_steps(Context* ctx, int nblk, double* A, int64_t lda, double* Dinv, int32_t* info, const Batch& bt,
                          int cbeg, int cend, const PotrfFwd& f = PotrfFwd()) {
-  const int mode = potrf_mode(ctx, nblk);
-  for_each_step(ctx, nblk, mode, cend, potrf_slots(ctx, bt.count), [&](int c, const StepPlan& s) {
+  const int mode = potrf_mode(ctx, nblk, bt.count);
+  for_each_step(ctx, nblk, bt.count, mode, cend, potrf_slots(ctx, bt.count), [&](int c, const StepPlan& s) {
     if (c < cbeg) return;
     const dim3 grid(s.tbase + s.ntrail + s.nsplit, bt.count);
     if (!f.r)
@@ -915,7 +920,7 @@ hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* 
   if (z_done) *z_done = false;
   PotrfFwd f;
   // the fold needs panels that apply exactly one pending column per launch (eager or lookahead schedules)
-  if (fr && fr->Y && fr->buf && (potrf_mode(ctx, nblk) == 1 || potrf_lazy(ctx, nblk) == 1)) {
+  if (fr && fr->Y && fr->buf && (potrf_mode(ctx, nblk, bt.count) == 1 || potrf_lazy(ctx, nblk, bt.count) == 1)) {
     const int64_t nr = rhs_row(fr->nrhs);
     f.Y = fr->Y;
     f.ldy = fr->ldy;

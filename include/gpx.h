@@ -137,8 +137,8 @@ size_t gpx_acq_params_size(void);
  *                          reports GPX_INFO_TIMEOUT (default 4194304; 0 = give up at the first unmet poll: tests)
  *  GPX_OPT_SWEEP_FUSED     1 (default) the fused small-n sweep where it applies (padded n <= 256), 0 the K* + trmm path
  *  GPX_OPT_GRAM_SPLIT      0 by size (default), else 1, 2 or 4 workgroups per 64x64 Gram tile
- *  GPX_OPT_POTRF_LAZY      multi-launch schedule: 0 by size (default), else flush the trailing update every g columns
- *  GPX_OPT_POTRF_MODE      multi-launch schedule: -1 by size (default), 0 eager panels, 1 lookahead panels */
+ *  GPX_OPT_POTRF_LAZY      multi-launch schedule: 0 by size and batch (default), else flush the trailing update every g columns
+ *  GPX_OPT_POTRF_MODE      multi-launch schedule: -1 by size and batch (default), 0 eager panels, 1 lookahead panels */
 enum {
   GPX_OPT_SPIN_LIMIT = 0,
   GPX_OPT_SWEEP_FUSED = 1,

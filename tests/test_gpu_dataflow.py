@@ -117,16 +117,24 @@ def test_options_from_environment_at_create():
 
 def test_fit_results_identical_across_pool_sizes(engine):
     """The schedule decides who runs a piece of work (the panel split depends on the co-resident slots a problem gets,
-    which a batch shares), never how a factor entry is computed: a batched fit of four problems equals the single fit
-    bit for bit at n = 4096."""
+    which a batch shares), never how a factor entry is computed: under one schedule (mode, lazy interval) a batched fit
+    of four problems equals the single fit bit for bit at n = 4096, for the single fit's default (eager) schedule and
+    the batch's default (lookahead, g = 6)."""
     n = 4096
     X, y = O.synthetic_problem(n, 8, 40)
     kp, _ = pair("rbf", 8, noise=1e-4)
-    st = engine.fit(t(X), t(y), kp)
-    L1 = st.L.cpu().numpy().copy()
-    sts = engine.fit_batched(t(np.stack([X] * 4)), t(np.stack([y] * 4)), kp)
-    for s in sts:
-        np.testing.assert_array_equal(np.tril(s.L.cpu().numpy()), np.tril(L1))
+    for mode, lazy in ((0, 1), (1, 6)):
+        engine.set_option("potrf_mode", mode)
+        engine.set_option("potrf_lazy", lazy)
+        try:
+            st = engine.fit(t(X), t(y), kp)
+            L1 = st.L.cpu().numpy().copy()
+            sts = engine.fit_batched(t(np.stack([X] * 4)), t(np.stack([y] * 4)), kp)
+        finally:
+            engine.set_option("potrf_mode", -1)
+            engine.set_option("potrf_lazy", 0)
+        for s in sts:
+            np.testing.assert_array_equal(np.tril(s.L.cpu().numpy()), np.tril(L1))
 
 
 def test_matrix_leading_dimension_limit(engine):

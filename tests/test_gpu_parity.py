@@ -471,7 +471,8 @@ def test_fit_batched_potrs_multiblock_owners(engine):
 
 def test_configs3_per_gpu_share_batched_n4096(engine):
     """BASELINE configs[3] (32 independent restarts x n=4096 d=8 over 8 GPUs) at its per-GPU share: 4 problems fitted in
-    the same launches (gpx_fit_batched_f64), each bit-identical to its own single fit, each with a 2^20-candidate logEI
+    the same launches (gpx_fit_batched_f64), each bit-identical to its own single fit under the batch's schedule
+    (lookahead panels, flush every 6 columns: the default for B >= 4 at 64 blocks), each with a 2^20-candidate logEI
     sweep checked by the full-size properties (device argmax = argmax of its scores, oracle re-score of the top-64 plus
     random candidates agrees on the winner and the values), then the records combined like the cross-GPU exchange
     (per-restart selection of optimize_acqf, /root/reference/optimization/Bayesian.py:105-112)."""
@@ -481,7 +482,13 @@ def test_configs3_per_gpu_share_batched_n4096(engine):
     sts = engine.fit_batched(t(np.stack([p[0] for p in probs])), t(np.stack([p[1] for p in probs])), kp)
     vals, idxs = [], []
     for b, (X, y) in enumerate(probs):
-        single = engine.fit(t(X), t(y), kp)
+        engine.set_option("potrf_mode", 1)
+        engine.set_option("potrf_lazy", 6)
+        try:
+            single = engine.fit(t(X), t(y), kp)
+        finally:
+            engine.set_option("potrf_mode", -1)
+            engine.set_option("potrf_lazy", 0)
         assert torch.equal(torch.tril(sts[b].L), torch.tril(single.L))
         engine.inverse(sts[b])
         engine.inverse(single)

@@ -3,6 +3,7 @@ rounds (median of the rounds), with the Gram / Cholesky / solve split from libgp
 alpha compared bit for bit with the first arm's.
 
   python tools/opt_ab.py --n 4096 --arms "potrf_half=0" "potrf_half=-1" "potrf_half=1"
+  python tools/opt_ab.py --n 4096 --batch 4 --arms "potrf_mode=0,potrf_lazy=1" "potrf_mode=1,potrf_lazy=2"  (fit_batched)
 """
 import argparse
 import os
@@ -21,15 +22,34 @@ ap.add_argument("--d", type=int, default=8)
 ap.add_argument("--kernel", default="rbf")
 ap.add_argument("--rounds", type=int, default=7)
 ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--batch", type=int, default=1)
 ap.add_argument("--arms", nargs="+", default=["potrf_half=0", "potrf_half=-1"])
 a = ap.parse_args()
 
-X, y = synthetic.problem(a.n, a.d, 0)
 dev = torch.device("cuda", 0)
 eng = GPEngine(dev)
 p = KernelParams(a.kernel, botorch_default_lengthscale(a.d), noise=1e-4)
-Xt, yt = torch.tensor(X, device=dev), torch.tensor(y, device=dev)
-st = eng.fit(Xt, yt, p)
+if a.batch > 1:
+    probs = [synthetic.problem(a.n, a.d, s) for s in range(a.batch)]
+    Xt = torch.stack([torch.tensor(X, device=dev) for X, _ in probs])
+    yt = torch.stack([torch.tensor(y, device=dev) for _, y in probs])
+
+
+    class _States(list):  # the problems' states, plus their stacked alpha for the bitwise comparison
+        pass
+
+    def fit(check, out):
+        sts = _States(eng.fit_batched(Xt, yt, p, check=check, out=out))
+        sts.alpha = torch.stack([s.alpha for s in sts])
+        return sts
+else:
+    X, y = synthetic.problem(a.n, a.d, 0)
+    Xt, yt = torch.tensor(X, device=dev), torch.tensor(y, device=dev)
+
+
+    def fit(check, out):
+        return eng.fit(Xt, yt, p, check=check, out=out)
+st = fit(True, None)
 torch.cuda.synchronize()
 names = ["gram", "potrf", "alpha"]
 eng.timing_enable(names)
@@ -53,12 +73,12 @@ for rnd in range(a.rounds):
             eng.set_option(k, v)
         for k, v in arm_opts(arm):
             eng.set_option(k, v)
-        st = eng.fit(Xt, yt, p, check=True, out=st)  # warm
+        st = fit(True, st)  # warm
         torch.cuda.synchronize()
         eng.timing_reset()
         t0 = time.perf_counter()
         for _ in range(a.reps):
-            st = eng.fit(Xt, yt, p, check=False, out=st)
+            st = fit(False, st)
         torch.cuda.synchronize()
         res[arm].append((time.perf_counter() - t0) / a.reps * 1e3)
         for k in names:
@@ -70,7 +90,7 @@ for rnd in range(a.rounds):
                 alpha0 = al
             same = bool(torch.equal(al, alpha0))
             rel = float((al - alpha0).abs().max() / alpha0.abs().max())
-            print(f"arm {arm!r}: alpha bitwise equal to arm 0: {same} (max rel diff {rel:.2e}); info {int(st.info.item())}")
+            print(f"arm {arm!r}: alpha bitwise equal to arm 0: {same} (max rel diff {rel:.2e}); info {int(st.info.max().item()) if a.batch == 1 else [int(x.info.item()) for x in st]}")
 for arm in a.arms:
     med = statistics.median(res[arm])
     split = ", ".join(f"{k} {statistics.median(parts[arm][k]):.4f}" for k in names)
