@@ -848,22 +848,29 @@ __global__ void __launch_bounds__(WG) potrf_dinv_kernel(double* __restrict__ A, 
 //              keeps g = 4 (3.165 vs 3.179 / 3.183 ms for g = 5 / 6) and n = 16384 g = 8 (30.16 vs 30.60 / 30.31 for
 //              g = 6 / 10);
 //   n = 16384: mode 1, g = 8 -> 31.4 ms (mode 0 g = 4: 34.4, g = 1: 46.3).
-// Batched fits share the co-resident slots, so the per-launch panel chain is hidden under more trailing work: at
-// n = 4096 (64 blocks) the lookahead schedule wins from two problems up (profiles/r04_batched_lazy_sweep.log, update ms
-// eager g = 1 -> mode 1 g = 4 / 6): B = 2 2.313 -> 2.186 / 2.207, B = 3 2.991 -> 2.784 / 2.792, B = 4 3.778 -> 3.326 /
-// 3.287, B = 8 6.92 -> 5.56 / 5.43; at n = 2048 the eager schedule stays best for B = 2 / 4 (B = 8: 1.314 vs 1.302).
+// Batched fits share the co-resident slots, so the per-launch panel chain is hidden under more trailing work and the
+// eager schedule's C traffic dominates: the lookahead schedule wins (profiles/r04_batched_lazy_sweep.log, update ms,
+// eager g = 1 -> mode 1 g = 4 / 6) at 64 blocks for B = 2 2.313 -> 2.186 / 2.207, B = 3 2.991 -> 2.784 / 2.792, B = 4
+// 3.778 -> 3.326 / 3.287, B = 8 6.92 -> 5.56 / 5.43; at 56 blocks B = 2 1.778 -> 1.739 / 1.744, B = 4 2.747 -> 2.543 /
+// 2.524; at 48 blocks B = 4 1.962 -> 1.895 / 1.863 (B = 2 1.350 -> 1.342, kept eager); at 40 and 32 blocks the eager
+// schedule stays best (B = 2 / 4).  At 128 blocks g = 8 beats 6 for B = 2 / 4 (9.28 vs 9.34, 16.37 vs 16.53 ms).
 // The handle options GPX_OPT_POTRF_LAZY / GPX_OPT_POTRF_MODE override.  Flushing every second launch only in the early,
 // trailing-bound launches and panel-wave priority were measured neutral (DESIGN.md §5, items 14 and the prio knob)
 // and are not offered.  Trailing tiles are dealt to the XCDs in 8 x 8 super-block chunks (trail_tile xmap = 1).
+static bool batched_lookahead(int nblk, int batch) {
+  return nblk <= 64 && ((batch >= 2 && nblk >= 56) || (batch >= 4 && nblk >= 48));
+}
+
 static int potrf_lazy(const Context* ctx, int nblk, int batch) {
   if (ctx->potrf_lazy > 0) return ctx->potrf_lazy;
-  if (nblk == 64 && batch >= 2) return batch >= 4 ? 6 : 4;
+  if (batched_lookahead(nblk, batch)) return batch >= 4 ? 6 : 4;
+  if (batch >= 2 && nblk > 100) return 8;
   return nblk > 128 ? 8 : (nblk > 100 ? 6 : (nblk > 64 ? 4 : 1));
 }
 
 static int potrf_mode(const Context* ctx, int nblk, int batch) {
   if (ctx->potrf_mode == 0 || ctx->potrf_mode == 1) return ctx->potrf_mode;
-  return nblk > 64 || (nblk == 64 && batch >= 2) ? 1 : 0;
+  return nblk > 64 || batched_lookahead(nblk, batch) ? 1 : 0;
 }
 
 // The plan of every launch c < cend (flush launches: c >= 1 and at least one interval after the previous flush).
