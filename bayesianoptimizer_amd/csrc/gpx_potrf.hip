@@ -853,7 +853,9 @@ __global__ void __launch_bounds__(WG) potrf_dinv_kernel(double* __restrict__ A, 
 // eager g = 1 -> mode 1 g = 4 / 6) at 64 blocks for B = 2 2.313 -> 2.186 / 2.207, B = 3 2.991 -> 2.784 / 2.792, B = 4
 // 3.778 -> 3.326 / 3.287, B = 8 6.92 -> 5.56 / 5.43; at 56 blocks B = 2 1.778 -> 1.739 / 1.744, B = 4 2.747 -> 2.543 /
 // 2.524; at 48 blocks B = 4 1.962 -> 1.895 / 1.863 (B = 2 1.350 -> 1.342, kept eager); at 40 and 32 blocks the eager
-// schedule stays best (B = 2 / 4).  At 128 blocks g = 8 beats 6 for B = 2 / 4 (9.28 vs 9.34, 16.37 vs 16.53 ms).
+// schedule stays best (B = 2 / 4).  At 80–96 blocks g = 6 beats 4 / 8 for B = 2 / 4 (n = 6144 B = 4: 8.09 vs 8.34 / 8.11,
+// B = 2: 4.86 vs 4.92 / 4.91; n = 5120 B = 4: 5.28 vs 5.41 / 5.30), at 128 blocks g = 8 beats 6 (B = 2: 9.28 vs 9.34,
+// B = 4: 16.37 vs 16.53 ms).
 // The handle options GPX_OPT_POTRF_LAZY / GPX_OPT_POTRF_MODE override.  Flushing every second launch only in the early,
 // trailing-bound launches and panel-wave priority were measured neutral (DESIGN.md §5, items 14 and the prio knob)
 // and are not offered.  Trailing tiles are dealt to the XCDs in 8 x 8 super-block chunks (trail_tile xmap = 1).
@@ -864,7 +866,7 @@ static bool batched_lookahead(int nblk, int batch) {
 static int potrf_lazy(const Context* ctx, int nblk, int batch) {
   if (ctx->potrf_lazy > 0) return ctx->potrf_lazy;
   if (batched_lookahead(nblk, batch)) return batch >= 4 ? 6 : 4;
-  if (batch >= 2 && nblk > 100) return 8;
+  if (batch >= 2 && nblk > 64) return nblk > 100 ? 8 : 6;
   return nblk > 128 ? 8 : (nblk > 100 ? 6 : (nblk > 64 ? 4 : 1));
 }
 
