@@ -875,14 +875,30 @@ static int potrf_mode(const Context* ctx, int nblk, int batch) {
   return nblk > 64 || batched_lookahead(nblk, batch) ? 1 : 0;
 }
 
+// A single fit of 64 blocks runs its first launches (c < 9) on the lookahead schedule with a flush every 4 columns and
+// switches to the eager schedule right after the flush at c = 8 (the eager launch c then applies column c - 1 to the
+// panels and the trailing matrix: every column is applied exactly once).  The early launches are bound by the eager
+// schedule's C traffic (launches 1-4: 39-42 us against ~17 us of panel chain, profiles/r04_potrf_launches_4096.log):
+// update 1.617 -> 1.596 ms at n = 4096 (profiles/r04_potrf_hybrid_ab.log; switch at c = 5 / 9 / 13 / 17 / 25 / 33 with
+// g = 4: 1.596 / 1.596-1.602 / 1.602 / 1.616 / 1.618 / 1.630 vs 1.616-1.619; g = 2 / 8 no better; the kept form 1.599 vs
+// 1.616).  Smaller fits keep the eager schedule throughout: the same switch at n = 2048 / 3072 / 3584 gave 0.683 / 1.058
+// / 1.325 vs 0.667 / 1.060 / 1.311 ms.
+static int potrf_switch(const Context* ctx, int nblk, int batch, int mode) {
+  if (ctx->potrf_mode >= 0 || ctx->potrf_lazy > 0 || mode != 0 || batch != 1) return 0;
+  return nblk == 64 ? 9 : 0;
+}
+constexpr int kSwitchLazy = 4;  // the flush interval before the switch (the switch launch follows a flush launch)
+
 // The plan of every launch c < cend (flush launches: c >= 1 and at least one interval after the previous flush).
 template <typename F>
 static void for_each_step(const Context* ctx, int nblk, int batch, int mode, int cend, int slots, F&& f) {
   const int g = potrf_lazy(ctx, nblk, batch);
+  const int sw = potrf_switch(ctx, nblk, batch, mode);
   int last = 0;
   for (int c = 0; c < cend; ++c) {
-    const bool flush = c >= 1 && c - last >= g;
-    f(c, step_plan(c, nblk, mode, last, flush, 1, slots));
+    const bool early = c < sw;
+    const bool flush = c >= 1 && c - last >= (early ? kSwitchLazy : g);
+    f(c, step_plan(c, nblk, early ? 1 : mode, last, flush, 1, slots));
     if (flush) last = c;
   }
 }
