@@ -883,22 +883,31 @@ static int potrf_mode(const Context* ctx, int nblk, int batch) {
 // g = 4: 1.596 / 1.596-1.602 / 1.602 / 1.616 / 1.618 / 1.630 vs 1.616-1.619; g = 2 / 8 no better; the kept form 1.599 vs
 // 1.616).  Smaller fits keep the eager schedule throughout: the same switch at n = 2048 / 3072 / 3584 gave 0.683 / 1.058
 // / 1.325 vs 0.667 / 1.060 / 1.311 ms.
-static int potrf_switch(const Context* ctx, int nblk, int batch, int mode) {
-  if (ctx->potrf_mode >= 0 || ctx->potrf_lazy > 0 || mode != 0 || batch != 1) return 0;
-  return nblk == 64 ? 9 : 0;
+// The other way round, a single fit above 64 blocks (lookahead schedule) switches to the eager schedule for its last
+// ~32 block columns (after the last flush launch before nblk - 32): there the trailing matrix is small and the eager
+// launches' panel chain is the shorter one (profiles/r04_potrf_eager_tail_ab.log: n = 8192 5.832 -> 5.720 ms with the
+// last 32, 5.811 -> 5.748 with 24, 5.796 -> 5.731 with 48; n = 16384 29.865 -> 29.715 with 32).
+constexpr int kEagerTail = 32;
+static int potrf_switch(const Context* ctx, int nblk, int batch, int mode, int g) {
+  if (ctx->potrf_mode >= 0 || ctx->potrf_lazy > 0 || batch != 1) return 0;
+  if (mode == 0) return nblk == 64 ? 9 : 0;
+  if (nblk - kEagerTail < g + 1) return 0;
+  return ((nblk - kEagerTail - 1) / g) * g + 1;
 }
 constexpr int kSwitchLazy = 4;  // the flush interval before the switch (the switch launch follows a flush launch)
 
-// The plan of every launch c < cend (flush launches: c >= 1 and at least one interval after the previous flush).
+// The plan of every launch c < cend (flush launches: c >= 1 and at least one interval after the previous flush);
+// launches c < sw (potrf_switch) run the lookahead schedule, the rest the eager one with a flush every launch.
 template <typename F>
 static void for_each_step(const Context* ctx, int nblk, int batch, int mode, int cend, int slots, F&& f) {
   const int g = potrf_lazy(ctx, nblk, batch);
-  const int sw = potrf_switch(ctx, nblk, batch, mode);
+  const int sw = potrf_switch(ctx, nblk, batch, mode, g);
+  const int ge = mode == 0 ? kSwitchLazy : g;
   int last = 0;
   for (int c = 0; c < cend; ++c) {
     const bool early = c < sw;
-    const bool flush = c >= 1 && c - last >= (early ? kSwitchLazy : g);
-    f(c, step_plan(c, nblk, early ? 1 : mode, last, flush, 1, slots));
+    const bool flush = c >= 1 && c - last >= (early ? ge : (sw > 0 ? 1 : g));
+    f(c, step_plan(c, nblk, early ? 1 : (sw > 0 ? 0 : mode), last, flush, 1, slots));
     if (flush) last = c;
   }
 }

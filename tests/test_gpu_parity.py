@@ -452,7 +452,8 @@ def test_fit_batched_matches_single_fits_and_oracle(engine, n, B, nrhs, inverse)
 def test_fit_batched_potrs_multiblock_owners(engine):
     """Batched factor-only fits where the solve's workgroups own several 128-row blocks each (gpx_potrs: G = 256 / B = 64
     workgroups per problem < nb = 65 blocks at n = 8320, B = 4; forward ascending then backward descending per
-    workgroup): alpha bit-identical to single fits (G = 65, one block each), and against the oracle's alpha."""
+    workgroup): alpha bit-identical to single fits under the same Cholesky schedule (G = 65, one block each), and
+    against the oracle's alpha."""
     n, d, B = 8320, 8, 4
     kp, op = pair("rbf", d, noise=1e-3)
     Xs, ys = [], []
@@ -462,7 +463,14 @@ def test_fit_batched_potrs_multiblock_owners(engine):
         ys.append(y)
     sts = engine.fit_batched(t(np.stack(Xs)), t(np.stack(ys)), kp)
     for b in (0, B - 1):
-        single = engine.fit(t(Xs[b]), t(ys[b]), kp)
+        # the batch's Cholesky schedule (lookahead, flush every 8; a single fit's default ends on the eager schedule)
+        engine.set_option("potrf_mode", 1)
+        engine.set_option("potrf_lazy", 8)
+        try:
+            single = engine.fit(t(Xs[b]), t(ys[b]), kp)
+        finally:
+            engine.set_option("potrf_mode", -1)
+            engine.set_option("potrf_lazy", 0)
         assert torch.equal(sts[b].alpha, single.alpha)
     a = sts[B - 1].alpha[:n].cpu().numpy().reshape(-1)
     a_r = O.fit(Xs[B - 1], ys[B - 1], op).alpha.reshape(-1)
