@@ -7,8 +7,10 @@ the engine fails loudly — there is no CPU fallback on the product path.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 import re
+import sys
 from ctypes import POINTER, c_char_p, c_double, c_int32, c_int64, c_size_t, c_void_p
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -26,9 +28,10 @@ GPX_OK, GPX_NOT_PD, GPX_INVALID_ARG, GPX_HIP_ERROR, GPX_RCCL_ERROR, GPX_TIMEOUT 
 STATUS_NAMES = {0: "OK", 1: "NOT_PD", 2: "INVALID_ARG", 3: "HIP_ERROR", 4: "RCCL_ERROR", 5: "TIMEOUT"}
 GPX_INFO_TIMEOUT = -(2 ** 31)  # device info word of a factorisation / solve whose in-launch hand-off timed out
 
-# per-handle options (include/gpx.h GPX_OPT_*)
-OPTIONS = {"spin_limit": 0, "sweep_fused": 1, "gram_split": 2, "potrf_lazy": 3, "potrf_mode": 4}
-GPX_OPT_COUNT = len(OPTIONS)
+# per-handle options (include/gpx.h GPX_OPT_*; slot 0 is GPX_OPT_RESERVED_0, the removed potrf_schedule)
+OPTIONS = {"spin_limit": 1, "sweep_fused": 2, "gram_split": 3, "potrf_lazy": 4, "potrf_mode": 5}
+GPX_OPT_RESERVED = (0,)
+GPX_OPT_COUNT = len(OPTIONS) + len(GPX_OPT_RESERVED)
 
 KERNEL_RBF, KERNEL_MATERN52, KERNEL_SCALE_LINEAR_MATERN52 = 0, 1, 2
 ACQ_EI, ACQ_LOGEI, ACQ_UCB, ACQ_VARIANCE = 0, 1, 2, 3
@@ -194,6 +197,8 @@ def load() -> ctypes.CDLL:
         raise GPXLibraryError(
             f"libgpx.so not found at {LIB_PATH}; build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "or `make -C bayesianoptimizer_amd/csrc` (hipcc --offload-arch=gfx950)")
+    if "GPX_LIB" in os.environ:  # A/B tooling only: say so, the product path never sets it
+        print(f"gpx: loading libgpx from GPX_LIB={LIB_PATH}", file=sys.stderr)
     try:
         lib = ctypes.CDLL(LIB_PATH)
     except OSError as e:  # pragma: no cover - depends on the ROCm runtime being present
@@ -209,6 +214,24 @@ def load() -> ctypes.CDLL:
             raise GPXLibraryError(f"{cls.__name__} is {ctypes.sizeof(cls)} bytes, libgpx expects {fn()}")
     _lib = lib
     return lib
+
+
+def source_sha256() -> str:
+    """sha256 over the library's sources as bayesianoptimizer_amd/csrc/Makefile stamps it into gpx_version(): every
+    csrc/*.cpp|*.hip|*.h sorted by name, then include/gpx.h, contents concatenated."""
+    csrc = os.path.join(_HERE, "csrc")
+    names = sorted(f for f in os.listdir(csrc) if f.endswith((".cpp", ".hip", ".h")))
+    h = hashlib.sha256()
+    for f in names + [HEADER_PATH]:
+        with open(os.path.join(csrc, f) if not os.path.isabs(f) else f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def library_source_sha256(lib=None) -> str:
+    """The source hash stamped into the loaded library's gpx_version() ('unstamped' for a build outside the Makefile)."""
+    v = (lib or load()).gpx_version().decode()
+    return v.rsplit(" src ", 1)[-1] if " src " in v else "unstamped"
 
 
 def header_symbols(path: str = HEADER_PATH):

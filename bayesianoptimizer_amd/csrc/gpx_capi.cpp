@@ -13,7 +13,12 @@ using gpx::Context;
 
 namespace {
 
-constexpr const char* kVersion = "gpx 0.1.0 (gfx950, fp64 MFMA)";
+// GPX_SOURCE_SHA256: sha256 over csrc/* and include/gpx.h (the Makefile stamps it; tests/test_capi.py recomputes it from
+// the working tree, so a stale or foreign libgpx.so is caught)
+#ifndef GPX_SOURCE_SHA256
+#define GPX_SOURCE_SHA256 "unstamped"
+#endif
+constexpr const char* kVersion = "gpx 0.5.0 (gfx950, fp64 MFMA) src " GPX_SOURCE_SHA256;
 
 gpx_status fail(Context* c, gpx_status st, const std::string& msg) {
   if (c) c->last_error = msg;
@@ -197,8 +202,9 @@ static gpx_status set_option(Context* c, int32_t option, int64_t v) {
 }
 
 static int option_by_name(const std::string& name) {
-  static const char* names[GPX_OPT_COUNT] = {"spin_limit", "sweep_fused", "gram_split", "potrf_lazy", "potrf_mode"};
-  for (int i = 0; i < GPX_OPT_COUNT; ++i)
+  // index = GPX_OPT_* number; slot 0 is reserved (the removed potrf_schedule) and has no name
+  static const char* names[GPX_OPT_COUNT] = {"", "spin_limit", "sweep_fused", "gram_split", "potrf_lazy", "potrf_mode"};
+  for (int i = 1; i < GPX_OPT_COUNT; ++i)
     if (name == names[i]) return i;
   return -1;
 }
@@ -216,7 +222,14 @@ static void apply_env_options(Context* c) {
     const size_t eq = item.find('=');
     if (eq != std::string::npos) {
       const int opt = option_by_name(item.substr(0, eq));
-      if (opt >= 0) (void)set_option(c, opt, std::atoll(item.c_str() + eq + 1));
+      if (opt >= 0) {
+        if (set_option(c, opt, std::atoll(item.c_str() + eq + 1)) != GPX_OK)
+          std::fprintf(stderr, "gpx: GPX_OPTIONS: %s (ignored)\n", c->last_error.c_str());
+      } else {
+        std::fprintf(stderr, "gpx: GPX_OPTIONS: unknown option '%s' (ignored)\n", item.substr(0, eq).c_str());
+      }
+    } else if (!item.empty()) {
+      std::fprintf(stderr, "gpx: GPX_OPTIONS: '%s' is not name=value (ignored)\n", item.c_str());
     }
     pos = end + 1;
   }

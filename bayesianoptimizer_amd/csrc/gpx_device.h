@@ -236,10 +236,19 @@ struct MfmaTile {
   // The same k loop accumulating onto the current acc.
   __device__ __forceinline__ void run_acc(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
                                           int64_t ldb, int kbeg, int kend, double* smem) {
+    run_acc_after(A, lda, B, ldb, kbeg, kend, smem, [] {});
+  }
+
+  // run_acc with after_first() called once the first k-tile's global loads are issued (e.g. loads that seed acc: issued
+  // behind the staging loads, so the first LDS store does not wait for them; kend > kbeg).
+  template <typename F>
+  __device__ __forceinline__ void run_acc_after(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
+                                                int64_t ldb, int kbeg, int kend, double* smem, F&& after_first) {
     if (kend <= kbeg) return;
     double* cur = smem;
     double* nxt = smem + BK * (PA + PB);
     load_regs(A, lda, B, ldb, kbeg);
+    after_first();
     store_lds(cur, cur + BK * PA);
     __syncthreads();
     for (int k0 = kbeg; k0 < kend; k0 += BK) {

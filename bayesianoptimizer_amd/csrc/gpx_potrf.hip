@@ -596,8 +596,31 @@ __device__ __forceinline__ void trail_tile(int t, int T, int M, int xmap, int& I
   I = J = 0;  // not reached: p < T
 }
 
+// acc = -C for an MfmaTile whose origin is C (row-major, leading dimension ld) through buffer loads: the lane's row / column
+// offset in one VGPR, each (i, r) row step wave-uniform (soffset) and each 16-column step an immediate, so the 64 seed loads
+// need no address registers.
+template <typename T>
+__device__ __forceinline__ void load_neg_c_buf(T& tl, rsrc_t rc, int64_t ld) {
+  const int v0 = (int)(((int64_t)T::row_of(0, 0) * ld + T::col_of(0)) * 8);
+#pragma unroll
+  for (int i = 0; i < T::WM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int so = (int)((int64_t)(16 * i + 4 * r) * ld * 8);
+#pragma unroll
+      for (int j = 0; j < T::WN; ++j)
+        tl.acc[i][j][r] = -__builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rc, v0 + 128 * j, so, 0));
+    }
+}
+
 // The 128 x TN tile with origin at 64-block (r0, q0): A -= sum_{k = k0}^{c-1} L_{r0..,k} L_{q0..,k}^T (TN = 128, or 64 for
-// the half tiles that end a long flush, StepPlan::nsplit; per element the same MFMA k order, so the same bits).
+// the half tiles that end a long flush, StepPlan::nsplit).
+// Schedule-invariant arithmetic: the accumulator is SEEDED with -C and every product added onto it in the k order of the
+// column blocks, so an element after columns k0..c-1 is the same MFMA chain whether those columns were applied one launch
+// at a time (eager), all at once (a lookahead flush), by the panel's own pre-update (seeded +C with the A operand negated:
+// round(C - ab) = -round(-C + ab)) or by a lookahead tile.  The factor, z and alpha are therefore bit-identical under every
+// schedule, batch size and GPX_OPT_POTRF_* option (tests/test_gpu_parity.py).  (Round 4 subtracted a from-zero product in
+// the epilogue, C - sum, whose rounding depended on how many columns a flush grouped.)
 template <int TN>
 __device__ __forceinline__ void trailing_tile_at(double* __restrict__ A, int64_t lda, int c, int k0, int cfirst, int r0,
                                                  int q0, double* lds) {
@@ -606,36 +629,20 @@ __device__ __forceinline__ void trailing_tile_at(double* __restrict__ A, int64_t
   double* C = A + (int64_t)r0 * NB * lda + (int64_t)q0 * NB;
   using TileT = MfmaTile<2 * NB, TN, 16, false, false>;
   TileT tl;
-  // C - acc, stored for the 64-blocks (rb, cb) with cb >= c+1 and rb >= cb, one row group i at a time: row group 0's C
-  // loads are issued before the last k-tile's MFMAs and group i+1's before group i's stores, so one load round trip is
-  // exposed instead of one per group (seeding acc with -C before the product, as the 64x64 panel updates do, pushes this
-  // 128x128 tile into 30 VGPR spills)
-  double cv[TileT::WN][4];
-  auto load_group = [&](int i) {
-#pragma unroll
-    for (int j = 0; j < TileT::WN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cv[j][r] = C[(int64_t)TileT::row_of(i, r) * lda + TileT::col_of(j)];
-  };
-  tl.zero();
-  tl.run_acc_peeled(Li, lda, Lj, lda, 0, (c - k0) * NB, lds, [&] { load_group(0); });
   const rsrc_t rc = buf_rsrc(C);
+  tl.run_acc_after(Li, lda, Lj, lda, 0, (c - k0) * NB, lds, [&] { load_neg_c_buf(tl, rc, lda); });
 #pragma unroll
   for (int i = 0; i < TileT::WM; ++i) {
-#pragma unroll
-    for (int j = 0; j < TileT::WN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) tl.acc[i][j][r] = cv[j][r] - tl.acc[i][j][r];
-    if (i + 1 < TileT::WM) load_group(i + 1);
-    // write-through 16-byte pairs; a 16-column pair never straddles a 64-block, and rows r = 0, 1 (even lanes) or 2, 3
-    // (odd lanes) of one lane lie in one 64-row block
+    // write-through 16-byte pairs of -acc; a 16-column pair never straddles a 64-block, and rows r = 0, 1 (even lanes) or
+    // 2, 3 (odd lanes) of one lane lie in one 64-row block
 #pragma unroll
     for (int j = 0; j < TileT::WN; ++j) {
       const int cb = q0 + (TileT::col_of(j) >> 6);
       const bool colok = cb >= cfirst;
       const bool k01 = colok && r0 + (TileT::row_of(i, 0) >> 6) >= cb;
       const bool k23 = colok && r0 + (TileT::row_of(i, 2) >> 6) >= cb;
-      store_block_pairs_sc1<TileT>(rc, lda, i, j, tl.acc[i][j], k01, k23);
+      const d4 v = -tl.acc[i][j];
+      store_block_pairs_sc1<TileT>(rc, lda, i, j, v, k01, k23);
     }
   }
 }

@@ -330,8 +330,11 @@ class GPEngine:
         self._check(self.lib.gpx_potrs_f64(
             self.handle, state.n, _ptr(state.L), state.L.stride(0), _ptr(state.Dinv), _ptr(Y), Y.stride(0), nrhs,
             float(state.params.const_mean), _ptr(alpha), _ptr(info), _ptr(ws), ws.numel()))
-        if int(info.item()) == _capi.GPX_INFO_TIMEOUT:
-            raise _capi.GPXTimeoutError("triangular solve hand-off timed out (GPX_OPT_SPIN_LIMIT)")
+        # a failed factor (info = pivot + 1, e.g. after fit(check=False)) leaves alpha untouched, a timed-out hand-off
+        # writes GPX_INFO_TIMEOUT: both raise instead of returning the uninitialised buffer
+        err = _capi.info_error(int(info.item()), "potrs")
+        if err is not None:
+            raise err
         return alpha
 
     def append(self, state: GPState, X, Y, check: bool = True, growth: float = 1.5) -> GPState:

@@ -12,8 +12,8 @@ These mirror the reference's operator surface for the hot path so calling code r
 Hyperparameters are either given (``params``) or fitted by maximum marginal likelihood with
 ``ExactGP.fit_hyperparameters`` (the fit_gpytorch_mll step of optimization/Bayesian.py:92-93,
 objective and gradient on the GPU, L-BFGS-B on the host; see mll.py).  NOT_PD handling follows the reference's
-jitter-retry policy (optimization/Bayesian6.py:481-488): the factorisation is retried with the jitters of
-``jitter_schedule`` before the NotPositiveDefiniteError propagates.
+jitter-retry policy (optimization/Bayesian6.py:481-488 through GPyTorch's psd_safe_cholesky, reference_jitter_schedule):
+the factorisation is retried with the jitters of ``jitter_schedule`` before the NotPositiveDefiniteError propagates.
 """
 from __future__ import annotations
 
@@ -22,9 +22,23 @@ from typing import Optional, Sequence
 
 import torch
 
-from ._capi import NotPositiveDefiniteError
+from ._capi import GPXTimeoutError, NotPositiveDefiniteError
 from .engine import KERNEL_KINDS, GPEngine, GPState, KernelParams, botorch_default_lengthscale
 from .transforms import Standardize
+
+
+def reference_jitter_schedule(jitter_val: float = 1e-4, retry: float = 1e-2, max_tries: int = 3) -> tuple:
+    """The diagonal jitters the reference's exact fit tries, in order (optimization/Bayesian6.py:482-488): GPyTorch's
+    psd_safe_cholesky [upstream] first factors without jitter, then adds cholesky_jitter x 10^i for i < max_tries
+    (settings.cholesky_max_tries = 3); the fit runs under cholesky_jitter(jitter_val = 1e-4, Bayesian6.py:66) and, if it
+    still fails, again under cholesky_jitter(1e-2).  The union in order: 0, 1e-4, 1e-3, 1e-2, 1e-1, 1."""
+    seq = [0.0]
+    for base in (jitter_val, retry):
+        for i in range(max_tries):
+            j = base * 10.0 ** i
+            if all(abs(j - s) > 1e-12 * j for s in seq):
+                seq.append(j)
+    return tuple(seq)
 
 
 @dataclass
@@ -38,7 +52,7 @@ class ExactGP:
 
     def __init__(self, train_X, train_Y, params: Optional[KernelParams] = None,
                  outcome_transform: Optional[Standardize] = None, engine=None,
-                 jitter_schedule: Sequence[float] = (0.0, 1e-4, 1e-2), capacity: int = 0):
+                 jitter_schedule: Optional[Sequence[float]] = None, capacity: int = 0):
         self.engine = engine if engine is not None else GPEngine()
         dev = getattr(self.engine, "device", None)
         X = torch.as_tensor(train_X, dtype=torch.float64)
@@ -51,11 +65,12 @@ class ExactGP:
         d = X.shape[1]
         self.params = params or KernelParams("rbf", botorch_default_lengthscale(d), noise=1e-4)
         self.outcome_transform = outcome_transform
-        self.jitter_schedule = tuple(jitter_schedule)
+        self.jitter_schedule = tuple(jitter_schedule) if jitter_schedule is not None else reference_jitter_schedule()
         self.capacity = int(capacity)  # training points the factor's buffers reserve room for (later appends)
         self.state: Optional[GPState] = None
         self.jitter_used = None
         self.mll_result = None
+        self.timeout_fallbacks = 0  # fits that fell back to the hand-off-free inverse path (see fit)
 
     @property
     def num_outputs(self) -> int:
@@ -65,17 +80,28 @@ class ExactGP:
     def lengthscale(self):
         return self.params.lengthscales(self.train_X.shape[1])
 
+    def _fit_once(self, Y, jit: float, inverse: bool):
+        cap = self.capacity if self.capacity > self.train_X.shape[0] else 0
+        return self.engine.fit(self.train_X, Y, self.params.replace(jitter=jit), capacity=cap, inverse=inverse)
+
     def fit(self) -> "ExactGP":
+        """Gram + Cholesky + alpha with the reference's jitter retry (NotPositiveDefiniteError -> next jitter,
+        optimization/Bayesian6.py:481-488).  The default update solves for alpha with one persistent launch whose
+        workgroups hand blocks to each other; if that hand-off times out (GPXTimeoutError: its workgroups could not all
+        become resident, e.g. beside a long kernel on another stream) the same jitter is refitted once through the
+        hand-off-free path (W = L^{-T} by multi-launch TRTRI, alpha = W W^T y), so a BO run never ends on a timeout -
+        the reference's fit has no such failure mode.  ``timeout_fallbacks`` counts those refits."""
         Y = self.train_Y
         if self.outcome_transform is not None:
             Y = self.outcome_transform.fit(Y).transform(Y)
         last = None
         for jit in self.jitter_schedule:
             try:
-                if self.capacity > self.train_X.shape[0]:
-                    self.state = self.engine.fit(self.train_X, Y, self.params.replace(jitter=jit), capacity=self.capacity)
-                else:
-                    self.state = self.engine.fit(self.train_X, Y, self.params.replace(jitter=jit))
+                try:
+                    self.state = self._fit_once(Y, jit, inverse=False)
+                except GPXTimeoutError:
+                    self.timeout_fallbacks += 1
+                    self.state = self._fit_once(Y, jit, inverse=True)
                 self.jitter_used = jit
                 return self
             except NotPositiveDefiniteError as e:  # reference: retry with larger cholesky_jitter

@@ -40,7 +40,7 @@ import torch
 
 from . import _capi
 from .engine import GPEngine, KernelParams
-from .models import ExactGP
+from .models import ExactGP, reference_jitter_schedule
 from .transforms import LogInputStandardizer, LogOutputStandardizer
 
 INPUT_COLUMNS = ("n", "eta", "sigma_y", "width", "height")  # simulator parameters, config/config.py order
@@ -284,7 +284,7 @@ class BayesianOptimizer:
         self._check_device_budget(n, n)
         self.x_tf = LogInputStandardizer(self._bounds_t()).fit(self.train_X)
         self.gp_model = ExactGP(self.x_tf(self.train_X), Ys, self._kernel_params(), engine=self.engine,
-                                jitter_schedule=(0.0, cfg.jitter_val, 1e-2))
+                                jitter_schedule=reference_jitter_schedule(cfg.jitter_val))
         if cfg.fit_hyperparameters:
             self.gp_model.fit_hyperparameters(cfg.prior_set, options=cfg.mll_options)
         else:
@@ -300,10 +300,10 @@ class BayesianOptimizer:
 
     def _free_device_bytes(self) -> Optional[int]:
         """Device memory a new factor can take: the driver's free memory plus what torch's caching allocator holds
-        unused (a factor released just before is still reserved there), or None off the GPU."""
+        unused (a factor released just before is still reserved there), or None off the GPU.  The cache is counted, not
+        emptied: releasing it every round would send the next fit's temporaries back through hipMalloc."""
         if not (torch.cuda.is_available() and getattr(self.gp_device, "type", "cpu") == "cuda"):
             return None
-        torch.cuda.empty_cache()
         free = torch.cuda.mem_get_info(self.gp_device)[0]
         return int(free + torch.cuda.memory_reserved(self.gp_device) - torch.cuda.memory_allocated(self.gp_device))
 
@@ -344,7 +344,7 @@ class BayesianOptimizer:
         cap = self._check_device_budget(n, cap)
         self.x_tf = LogInputStandardizer(self._bounds_t()).fit(self.train_X)
         Xs = self.x_tf(self.train_X)
-        jit = (0.0, cfg.jitter_val, 1e-2)
+        jit = reference_jitter_schedule(cfg.jitter_val)
         if cfg.fit_hyperparameters:
             m = int(self.svgp_threshold)
             sub = np.sort(self._subsample_rng.choice(n, size=m, replace=False))

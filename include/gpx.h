@@ -132,7 +132,13 @@ size_t gpx_acq_params_size(void);
 
 /* Per-handle options (tuning and diagnostics; every default is the measured best).  gpx_create reads the environment
  * variable GPX_OPTIONS once ("name=value,name=value", names as below in lower case without the prefix, e.g.
- * "sweep_fused=0,potrf_mode=1"); nothing else in the library reads the environment.
+ * "sweep_fused=0,potrf_mode=1"; an unknown name is reported on stderr and ignored); nothing else in the library reads
+ * the environment.  The numbers are stable ABI: a removed option keeps its slot as GPX_OPT_RESERVED_n, which
+ * gpx_set_option / gpx_get_option reject with GPX_INVALID_ARG.  None of the options changes a result bit: the Cholesky
+ * schedules are arithmetic-invariant (any schedule that folds the forward substitution - every default, and every
+ * potrf_mode 1 or potrf_lazy 1 setting - gives the same L, z and alpha; potrf_mode 0 with potrf_lazy > 1 runs the
+ * forward substitution as a separate solve, so only alpha's rounding differs there).
+ *  GPX_OPT_RESERVED_0      (was GPX_OPT_POTRF_SCHEDULE, removed in 0.4)
  *  GPX_OPT_SPIN_LIMIT      polls before an in-launch hand-off (the triangular solve's) gives up and
  *                          reports GPX_INFO_TIMEOUT (default 4194304; 0 = give up at the first unmet poll: tests)
  *  GPX_OPT_SWEEP_FUSED     1 (default) the fused small-n sweep where it applies (padded n <= 256), 0 the K* + trmm path
@@ -140,12 +146,13 @@ size_t gpx_acq_params_size(void);
  *  GPX_OPT_POTRF_LAZY      multi-launch schedule: 0 by size and batch (default), else flush the trailing update every g columns
  *  GPX_OPT_POTRF_MODE      multi-launch schedule: -1 by size and batch (default), 0 eager panels, 1 lookahead panels */
 enum {
-  GPX_OPT_SPIN_LIMIT = 0,
-  GPX_OPT_SWEEP_FUSED = 1,
-  GPX_OPT_GRAM_SPLIT = 2,
-  GPX_OPT_POTRF_LAZY = 3,
-  GPX_OPT_POTRF_MODE = 4,
-  GPX_OPT_COUNT = 5
+  GPX_OPT_RESERVED_0 = 0,
+  GPX_OPT_SPIN_LIMIT = 1,
+  GPX_OPT_SWEEP_FUSED = 2,
+  GPX_OPT_GRAM_SPLIT = 3,
+  GPX_OPT_POTRF_LAZY = 4,
+  GPX_OPT_POTRF_MODE = 5,
+  GPX_OPT_COUNT = 6
 };
 gpx_status gpx_set_option(gpx_handle h, int32_t option, int64_t value);
 gpx_status gpx_get_option(gpx_handle h, int32_t option, int64_t* value_host);
@@ -219,8 +226,10 @@ gpx_status gpx_fit_factor_f64(gpx_handle h, const gpx_kernel_params* p, int64_t 
 /* Batched posterior updates: `batch` independent problems of the same n, d and kernel parameters (restarts /
  * seeds: BASELINE configs[3], the per-batch `info` of the SURVEY §8b proposal) in the SAME launches, the problem
  * index being one more grid dimension.  Every array of problem b starts at base + b * stride_* (element strides,
- * >= one problem); info: device int32[batch], each 0 or that problem's failing pivot + 1.  Results are identical to
- * `batch` calls of gpx_fit_f64.  The Cholesky is a latency-bound chain of nblk dependent launches, so a batch of B
+ * >= one problem); info: device int32[batch], each 0 or that problem's failing pivot + 1.  Results are identical bit for
+ * bit to `batch` calls of gpx_fit_f64 with the default options, although the batch may take a different Cholesky
+ * schedule (every schedule computes each factor entry by the same MFMA chain, gpx_potrf.hip trailing_tile_at), so a
+ * problem's result does not depend on how many problems share its GPU.  The Cholesky is a latency-bound chain of nblk dependent launches, so a batch of B
  * costs far less than B fits (replaces the per-restart fits of optimize_acqf / fit_gpytorch_mll restarts [upstream]). */
 gpx_status gpx_fit_batched_workspace_size(int64_t n, int64_t nrhs, int64_t batch, size_t* bytes);
 gpx_status gpx_fit_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n, const double* X,

@@ -230,6 +230,34 @@ def fit(X: np.ndarray, y: np.ndarray, p: KernelParams) -> GPState:
     return GPState(X=X, L=L, alpha=alpha, params=p)
 
 
+def psd_safe_jitters(jitter_val: float = 1e-4, retry: float = 1e-2, max_tries: int = 3):
+    """Jitters the reference's exact fit tries in order (optimization/Bayesian6.py:482-488): GPyTorch's
+    psd_safe_cholesky [upstream] factors without jitter, then with cholesky_jitter * 10^i, i < cholesky_max_tries = 3,
+    under cholesky_jitter(jitter_val = 1e-4) (Bayesian6.py:66,483) and on failure under cholesky_jitter(1e-2) (:487)."""
+    seq = [0.0]
+    for base in (jitter_val, retry):
+        for i in range(max_tries):
+            j = base * 10.0 ** i
+            if all(abs(j - s) > 1e-12 * j for s in seq):
+                seq.append(j)
+    return seq
+
+
+def fit_with_jitter(X: np.ndarray, y: np.ndarray, p: KernelParams, jitters=None):
+    """fit() with the first jitter of ``jitters`` (default psd_safe_jitters()) whose factorisation succeeds; returns
+    (state, jitter, failed pivots of the earlier attempts).  Raises the last NotPDError when none succeeds."""
+    failed = []
+    last = None
+    for jit in (psd_safe_jitters() if jitters is None else jitters):
+        q = KernelParams(**{**p.__dict__, "jitter": jit})
+        try:
+            return fit(X, y, q), jit, failed
+        except NotPDError as e:
+            failed.append(e.pivot)
+            last = e
+    raise last
+
+
 def append(state: GPState, X_all: np.ndarray, y_all: np.ndarray) -> GPState:
     """Incremental posterior update: the rows of X_all past ``state.X`` appended by a bordered
     Cholesky (L21 = K21 L11^{-T}, L22 = chol(K22 - L21 L21^T)) instead of the refit the reference runs every round

@@ -9,6 +9,13 @@ Fixtures are data (inputs and oracle outputs), never reference source:
                 scored on 512 rows of validation_set.csv
   real_b7_*     the same rows through Bayesian7's input transform (optimization/Bayesian7.py:181-190,363-385),
                 RBF kernel
+  results_*     the INPUTS of the reference's own results files at full size (results/optimization_results*.csv:
+                physical X, 5 columns, and the 8 raw outputs, read by column position because two files name their
+                outputs disp_* instead of x_*), and validation_2048 the first 2048 rows of validation_set.csv.  No
+                expected outputs: tests/test_gpu_realdata.py runs the oracle on them on the GPU box's host.
+                optimization_results2.csv row 2386 (1-based data row 2385) holds a corrupt field
+                ("200.067 7064061164856"): that row is dropped and listed in `dropped` (the reference's own resume,
+                optimization/Bayesian7.py:274-286, would fail to parse the whole file).
 The reference's CSVs are read only here (at generation time); the .npz files carry the numbers.
 """
 from __future__ import annotations
@@ -95,10 +102,41 @@ def real(ref: str):
     save("real_b7_results256_val512", Xs7, Y7, Xv7, p7)
 
 
+RESULTS_FILES = {  # tag -> file under results/ 
+    "r3000": "optimization_results.csv",
+    "r3901": "optimization_results1.csv",
+    "r4235": "optimization_results1012.csv",
+    "r5000": "optimization_results2.csv",
+    "r7740": "optimization_results1009.csv",
+}
+
+
+def results_inputs(ref: str):
+    import pandas as pd
+
+    for tag, fname in RESULTS_FILES.items():
+        df = pd.read_csv(os.path.join(ref, "results", fname))
+        num = df.apply(lambda c: pd.to_numeric(c, errors="coerce")).to_numpy(np.float64)
+        bad = np.flatnonzero(np.isnan(num).any(axis=1))
+        num = np.delete(num, bad, axis=0)
+        X, Y = num[:, :5], num[:, 5:13]
+        dup = X.shape[0] - np.unique(X, axis=0).shape[0]
+        np.savez_compressed(os.path.join(HERE, f"results_{tag}.npz"), X=X, Y=Y, source=np.array(fname),
+                            dropped=bad.astype(np.int64), duplicate_rows=np.int64(dup))
+        print("wrote", tag, fname, X.shape, "dropped", bad.tolist(), "duplicate X rows", dup)
+    dv = pd.read_csv(os.path.join(ref, "validation_set.csv")).iloc[:2048].to_numpy(np.float64)
+    np.savez_compressed(os.path.join(HERE, "validation_2048.npz"), X=dv[:, :5], Y=dv[:, 5:13])
+    print("wrote validation_2048", dv.shape)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
+    ap.add_argument("--only-results", action="store_true", help="write only the results_* / validation fixtures")
     a = ap.parse_args()
-    synthetic()
+    if not a.only_results:
+        synthetic()
     if os.path.isdir(a.reference):
-        real(a.reference)
+        if not a.only_results:
+            real(a.reference)
+        results_inputs(a.reference)

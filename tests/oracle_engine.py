@@ -39,7 +39,7 @@ class OracleEngine:
     def __init__(self):
         self.calls = {"fit": 0, "posterior": 0, "acquire": 0}
 
-    def fit(self, X, Y, params, check=True, out=None, capacity=0):
+    def fit(self, X, Y, params, check=True, out=None, capacity=0, inverse=False):
         self.calls["fit"] += 1
         self.calls["fit_n"] = self.calls.get("fit_n", []) + [int(np.asarray(X).shape[0])]
         X = torch.as_tensor(X, dtype=torch.float64).cpu().numpy()

@@ -40,6 +40,13 @@ def test_version_and_padding(lib):
         assert lib.gpx_padded_n(n) == p
 
 
+def test_loaded_library_is_built_from_this_tree(lib):
+    """Binary provenance (VERDICT r4 item 7): the Makefile stamps a sha256 of csrc/* + include/gpx.h into gpx_version();
+    the library the tests load must carry the hash of the working tree's sources, not an A/B or stale build."""
+    assert _capi.library_source_sha256(lib) == _capi.source_sha256(), lib.gpx_version().decode()
+
+
+
 def test_struct_layout_matches_header():
     # gpx_kernel_params: 2 int32 + 2*32 doubles + 4 doubles + 2 int32
     assert ctypes.sizeof(_capi.KernelParamsC) == 8 + 2 * 32 * 8 + 4 * 8 + 8
@@ -58,11 +65,13 @@ def test_header_constants_match_python():
                       ("GPX_ACQ_EI", 0), ("GPX_ACQ_LOGEI", 1), ("GPX_ACQ_UCB", 2), ("GPX_ACQ_VARIANCE", 3),
                       ("GPX_TIMER_TRMM", 5)]:
         assert re.search(rf"\b{name} = {val}\b", hdr), name
-    # the per-handle option numbering the binding uses (the dead potrf_schedule slot was removed in round 4)
+    # the per-handle option numbering the binding uses: stable ABI numbers, the removed potrf_schedule keeps slot 0 as
+    # GPX_OPT_RESERVED_0 (round 4 had renumbered the enum without an ABI bump)
     for name, val in _capi.OPTIONS.items():
         assert re.search(rf"\bGPX_OPT_{name.upper()} = {val}\b", hdr), name
+    assert _capi.OPTIONS["spin_limit"] == 1 and _capi.OPTIONS["potrf_mode"] == 5
+    assert re.search(r"\bGPX_OPT_RESERVED_0 = 0\b", hdr)
     assert re.search(rf"\bGPX_OPT_COUNT = {_capi.GPX_OPT_COUNT}\b", hdr)
-    assert "POTRF_SCHEDULE" not in hdr
 
 
 def test_workspace_queries_without_gpu(lib):

@@ -73,3 +73,42 @@ def test_dropin_crosses_svgp_threshold_on_gpu(tmp_path, engine):
     # the parity scale of a variance is the prior variance k(x, x) >= outputscale, not the posterior
     # variance, which at 3050 points is ~1e-6 (bordered update vs refit measured 4.6e-12 absolute)
     assert (a.variance - b.variance).abs().max() <= 1e-9 * gp.params.outputscale
+
+
+def test_dropin_survives_timed_out_handoffs(tmp_path, engine):
+    """with spin_limit = 0 every in-launch hand-off of the persistent backward solve times out.
+    ExactGP.fit then refits the same jitter through the hand-off-free inverse path (multi-launch TRTRI, alpha = W W^T y),
+    so BayesianOptimizer.optimize() runs to completion (the reference's fit, optimization/Bayesian6.py:482-488, has no
+    such failure mode) and the final model's alpha and posterior equal the oracle's."""
+    from oracle import gp_oracle as O
+    from tests.oracle_engine import to_oracle_params
+
+    cfg = GPConfig(fit_hyperparameters=False, incremental_updates=False, raw_samples=4096)
+    sim = StubSimulator()
+    engine.set_option("spin_limit", 0)
+    try:
+        opt = BayesianOptimizer(sim, BOUNDS, str(tmp_path / "to"), n_initial_points=600, n_batches=2, batch_size=8,
+                                target_total=616, engine=engine, gp_config=cfg, acquisition="logei", seed=5)
+        best_params, best_value = opt.optimize()
+        opt.fit_gp_model()
+        gp = opt.gp_model
+        assert gp.timeout_fallbacks >= 1  # 600+ points: 5+ row blocks, so the solve has hand-offs to time out
+        X = gp.train_X.cpu().numpy()
+        Y = gp.train_Y.cpu().numpy()
+        a = gp.state.alpha[: X.shape[0]].cpu().numpy()
+    finally:
+        engine.set_option("spin_limit", 1 << 22)
+        sim.cleanup()
+    assert np.isfinite(best_value) and best_params.shape == (5,)
+    data = np.loadtxt(tmp_path / "to" / "optimization_results.csv", delimiter=",", skiprows=1)
+    assert data.shape[0] == 616
+    ost = O.fit(X, Y, to_oracle_params(gp.params.replace(jitter=gp.jitter_used), X.shape[1]))
+    ar = ost.alpha.reshape(a.shape)
+    assert np.abs(a - ar).max() <= 1e-8 * np.abs(ar).max()
+    Xq = np.random.default_rng(1).random((64, X.shape[1]))
+    post = gp.posterior(torch.tensor(Xq, device=engine.device))
+    mu_r, _ = O.posterior(ost, Xq)
+    mu_r = mu_r.reshape(64, -1)
+    assert gp.outcome_transform is None  # the drop-in standardises the targets itself (Bayesian7.py:363-385)
+    mu = post.mean.cpu().numpy()
+    assert np.abs(mu - mu_r).max() <= 1e-9 * np.abs(mu_r).max()

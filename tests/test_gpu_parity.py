@@ -452,7 +452,7 @@ def test_fit_batched_matches_single_fits_and_oracle(engine, n, B, nrhs, inverse)
 def test_fit_batched_potrs_multiblock_owners(engine):
     """Batched factor-only fits where the solve's workgroups own several 128-row blocks each (gpx_potrs: G = 256 / B = 64
     workgroups per problem < nb = 65 blocks at n = 8320, B = 4; forward ascending then backward descending per
-    workgroup): alpha bit-identical to single fits under the same Cholesky schedule (G = 65, one block each), and
+    workgroup): alpha bit-identical to default single fits (G = 65, one block each; a different Cholesky schedule), and
     against the oracle's alpha."""
     n, d, B = 8320, 8, 4
     kp, op = pair("rbf", d, noise=1e-3)
@@ -463,14 +463,9 @@ def test_fit_batched_potrs_multiblock_owners(engine):
         ys.append(y)
     sts = engine.fit_batched(t(np.stack(Xs)), t(np.stack(ys)), kp)
     for b in (0, B - 1):
-        # the batch's Cholesky schedule (lookahead, flush every 8; a single fit's default ends on the eager schedule)
-        engine.set_option("potrf_mode", 1)
-        engine.set_option("potrf_lazy", 8)
-        try:
-            single = engine.fit(t(Xs[b]), t(ys[b]), kp)
-        finally:
-            engine.set_option("potrf_mode", -1)
-            engine.set_option("potrf_lazy", 0)
+        # the default single fit (lookahead then the eager tail) against the batch's default (lookahead, flush every 8):
+        # the same bits (schedule-invariant arithmetic)
+        single = engine.fit(t(Xs[b]), t(ys[b]), kp)
         assert torch.equal(sts[b].alpha, single.alpha)
     a = sts[B - 1].alpha[:n].cpu().numpy().reshape(-1)
     a_r = O.fit(Xs[B - 1], ys[B - 1], op).alpha.reshape(-1)
@@ -479,8 +474,8 @@ def test_fit_batched_potrs_multiblock_owners(engine):
 
 def test_configs3_per_gpu_share_batched_n4096(engine):
     """BASELINE configs[3] (32 independent restarts x n=4096 d=8 over 8 GPUs) at its per-GPU share: 4 problems fitted in
-    the same launches (gpx_fit_batched_f64), each bit-identical to its own single fit under the batch's schedule
-    (lookahead panels, flush every 6 columns: the default for B >= 4 at 64 blocks), each with a 2^20-candidate logEI
+    the same launches (gpx_fit_batched_f64; lookahead panels, flush every 6 columns), each bit-identical to its own
+    default single fit (lookahead start, then eager), each with a 2^20-candidate logEI
     sweep checked by the full-size properties (device argmax = argmax of its scores, oracle re-score of the top-64 plus
     random candidates agrees on the winner and the values), then the records combined like the cross-GPU exchange
     (per-restart selection of optimize_acqf, /root/reference/optimization/Bayesian.py:105-112)."""
@@ -490,13 +485,7 @@ def test_configs3_per_gpu_share_batched_n4096(engine):
     sts = engine.fit_batched(t(np.stack([p[0] for p in probs])), t(np.stack([p[1] for p in probs])), kp)
     vals, idxs = [], []
     for b, (X, y) in enumerate(probs):
-        engine.set_option("potrf_mode", 1)
-        engine.set_option("potrf_lazy", 6)
-        try:
-            single = engine.fit(t(X), t(y), kp)
-        finally:
-            engine.set_option("potrf_mode", -1)
-            engine.set_option("potrf_lazy", 0)
+        single = engine.fit(t(X), t(y), kp)
         assert torch.equal(torch.tril(sts[b].L), torch.tril(single.L))
         engine.inverse(sts[b])
         engine.inverse(single)
@@ -523,6 +512,42 @@ def test_configs3_per_gpu_share_batched_n4096(engine):
     gv, gi = engine.argmax_combine(torch.tensor(vals, dtype=torch.float64), torch.tensor(idxs))
     ref_v, ref_i = O.combine_argmax(list(zip(vals, idxs)))
     assert (float(gv.item()), int(gi.item())) == (ref_v, ref_i)
+
+
+def test_configs3_selection_independent_of_problems_per_gpu(engine):
+    """the 32 restarts of BASELINE configs[3] land 4 per GPU on 8 GPUs but 32 per GPU on one, so a
+    restart's factor must not depend on how many problems share its launches.  Eight n = 4096 problems are fitted as
+    8 x B=1, 4 x B=2, 2 x B=4 and 1 x B=8, each swept over 2^16 logEI candidates; every layout must give the same
+    per-restart (value, index) records bit for bit and the same combined winner (restart selection of optimize_acqf,
+    /root/reference/optimization/Bayesian.py:105-112).  The margin between the winner and the runner-up is reported."""
+    n, d, m, P = 4096, 8, 1 << 16, 8
+    kp, _ = pair("rbf", d, noise=1e-4)
+    probs = [O.synthetic_problem(n, d, 500 + b) for b in range(P)]
+    Xs = [t(O.sobol_candidates(m, d, 900 + b)) for b in range(P)]
+    best_f = [float(y.max()) for _, y in probs]
+    layouts = {}
+    for B in (1, 2, 4, 8):
+        recs = []
+        for g0 in range(0, P, B):
+            grp = probs[g0:g0 + B]
+            if B == 1:
+                sts = [engine.fit(t(grp[0][0]), t(grp[0][1]), kp)]
+            else:
+                sts = engine.fit_batched(t(np.stack([p[0] for p in grp])), t(np.stack([p[1] for p in grp])), kp)
+            for j, st in enumerate(sts):
+                b = g0 + j
+                bv, bi = engine.acquire(st, Xs[b], "logei", best_f=best_f[b], index_offset=b * m)
+                recs.append((float(bv.item()), int(bi.item())))
+            del sts
+        layouts[B] = recs
+    for B in (2, 4, 8):
+        assert layouts[B] == layouts[1], B
+    vals = sorted((v for v, _ in layouts[1]), reverse=True)
+    win = O.combine_argmax(layouts[1])
+    gv, gi = engine.argmax_combine(torch.tensor([v for v, _ in layouts[1]], dtype=torch.float64),
+                                   torch.tensor([i for _, i in layouts[1]]))
+    assert (float(gv.item()), int(gi.item())) == win
+    print(f"configs[3] winner restart {win[1] // m} index {win[1] % m}, margin to runner-up {vals[0] - vals[1]:.3e}")
 
 
 def test_fit_batched_reports_not_pd_per_problem(engine):

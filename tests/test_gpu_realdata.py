@@ -1,0 +1,135 @@
+"""Parity on the reference's own data at full size (SURVEY §7 "near-duplicate real X").
+
+Inputs: the five results files of /root/reference/results (3000, 3901, 4235, 5000 and 7740 rows; the 7740-row
+optimization_results1009.csv holds 1550 duplicate X rows) and the first 2048 rows of validation_set.csv, committed as
+data under tests/golden/results_*.npz / validation_2048.npz (tests/golden/make_golden.py results_inputs).  The model is
+the exact-GP mode of optimization/Bayesian6.py:458-490:
+  * X in the unit cube of the physical bounds (config/config.py:2-20), Y = log(Y_raw + shift) standardised per output
+    (Bayesian6.py:421-443, 463-468), all 8 outputs sharing one factorisation;
+  * covariance ScaleKernel(LinearKernel(ARD) + MaternKernel(2.5, ARD)) (Bayesian6.py:471-473) with fixed
+    hyperparameters (the reference fits them with fit_gpytorch_mll; that optimiser is not the object of this test);
+  * NOT_PD handling: the jitters GPyTorch's psd_safe_cholesky tries under cholesky_jitter(1e-4), then the retry under
+    cholesky_jitter(1e-2) (Bayesian6.py:482-488): 0, 1e-4, 1e-3, 1e-2, 1e-1, 1.  The GPU (ExactGP.fit) and the oracle
+    (SciPy LAPACK on the box's host, oracle.gp_oracle.fit_with_jitter) must settle on the same jitter.  At noise 1e-4 (the
+    likelihood's floor) every file factors without jitter; the noise-free fit of the 1550-duplicate file fails at jitter 0
+    in both and is taken at 1e-4.
+Checked: alpha, mu / sigma^2 of all outputs at the 2048 validation points at the parity tolerance (|d mu| <= 1e-9
+max|mu|, |d var| <= 1e-9 k(x, x); cond(K) is ~2e7 here and the oracle's own distance-form choice moves mu by ~3e-12
+relative), the variance-sum top-256 (Bayesian7.py:664-681's score and torch.topk, through gpx_topk_f64)
+and the logEI argmax index bit for bit (near-ties within the error bound are reported, never silently accepted).
+"""
+import os
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from bayesianoptimizer_amd import KernelParams
+from bayesianoptimizer_amd.models import ExactGP, reference_jitter_schedule
+from oracle import gp_oracle as O
+from tests.conftest import GOLDEN
+from tests.test_gpu_parity import check_argmax, check_posterior, t
+
+pytestmark = pytest.mark.gpu
+
+BOUNDS = np.array([(0.3, 1.0), (0.001, 300.0), (0.001, 400.0), (2.0, 7.0), (2.0, 7.0)])  # config/config.py:2-20
+LS, OS, LINVAR = 0.4, 1.5, np.linspace(0.05, 0.45, 5)
+
+
+def load(tag):
+    z = np.load(os.path.join(GOLDEN, f"results_{tag}.npz"))
+    return z["X"], z["Y"], int(z["duplicate_rows"])
+
+
+def unit(X):
+    return (X - BOUNDS[:, 0]) / (BOUNDS[:, 1] - BOUNDS[:, 0])
+
+
+def bayesian6_targets(Y):
+    """log(Y + shift) standardised per output (optimization/Bayesian6.py:421-443, 463-468)."""
+    eps = max(1e-12, np.abs(Y).max() * 1e-6)
+    shift = (-Y.min() + eps) if Y.min() <= 0.0 else eps
+    Yl = np.log(Y + shift)
+    return (Yl - Yl.mean(0)) / np.maximum(Yl.std(0, ddof=1), 1e-12)
+
+
+@pytest.mark.parametrize("tag,noise", [("r3000", 1e-4), ("r3901", 1e-4), ("r4235", 1e-4), ("r5000", 1e-4),
+                                       ("r7740", 1e-4), ("r7740", 0.0)])
+def test_reference_results_full_size(engine, tag, noise):
+    t0 = time.time()
+    X, Yraw, dups = load(tag)
+    Xu, Y6 = unit(X), bayesian6_targets(Yraw)
+    Xv = unit(np.load(os.path.join(GOLDEN, "validation_2048.npz"))["X"])
+    n, d = Xu.shape
+    kp = KernelParams("scale_linear_matern52", LS, outputscale=OS, noise=noise, linear_variance=LINVAR)
+    op = O.KernelParams(O.SCALE_LINEAR_MATERN52, np.full(d, LS), outputscale=OS, noise=noise, linear_variance=LINVAR)
+    gp = ExactGP(Xu, Y6, kp, engine=engine).fit()
+    assert gp.jitter_schedule == tuple(O.psd_safe_jitters()) == reference_jitter_schedule()
+    ost, jit, failed = O.fit_with_jitter(Xu, Y6, op)
+    assert gp.jitter_used == jit, f"GPU took jitter {gp.jitter_used}, oracle {jit} (oracle failed at pivots {failed})"
+    if noise == 0.0:
+        assert dups > 0 and jit > 0.0, "the noise-free duplicate file must need the jitter retry"
+    a = gp.state.alpha[:n].cpu().numpy()
+    ar = ost.alpha.reshape(n, -1)
+    assert np.abs(a - ar).max() <= 1e-8 * np.abs(ar).max()
+    mu, var = engine.posterior(gp.state, t(Xv))
+    mu_g, var_g = mu.cpu().numpy(), var.cpu().numpy()
+    mu_r, var_r = O.posterior(ost, Xv)
+    check_posterior(mu_g, var_g, mu_r, var_r, O.kernel_diag(Xv, op))
+    # variance-sum score of the pool scan (all outputs share the kernel, so the sum orders like one variance)
+    s_g = torch.tensor(var_g * Y6.shape[1], dtype=torch.float64, device=engine.device)
+    s_r = var_r * Y6.shape[1]
+    k = 256
+    _, idx = engine.topk(s_g, k)
+    ref_idx = O.topk_desc(s_r, k)
+    ref_idx = ref_idx[1] if isinstance(ref_idx, tuple) else ref_idx
+    got = idx.cpu().numpy()
+    if not np.array_equal(got, np.asarray(ref_idx)):
+        bad = int(np.flatnonzero(got != np.asarray(ref_idx))[0])
+        gap = abs(s_r[got[bad]] - s_r[ref_idx[bad]])
+        pytest.fail(f"{tag}: top-{k} differs at rank {bad} (gpu {got[bad]}, oracle {ref_idx[bad]}, score gap {gap:.3e})")
+    # logEI argmax of output 0 over the validation points (Bayesian.py:96-113 on a fixed grid)
+    best_f = float(Y6[:, 0].max())
+    _, bi, sc = engine.acquire(gp.state, t(Xv), "logei", best_f=best_f, return_scores=True)
+    sref = O.acquisition(mu_r.reshape(len(Xv), -1)[:, 0], var_r, O.ACQ_LOGEI, best_f)
+    check_argmax(int(bi.item()), sref, sc.cpu().numpy(), f"{tag} logEI")
+    print(f"{tag} n={n} noise={noise} jitter={jit} (oracle failed pivots {failed[:3]}) dup={dups} "
+          f"|dmu|/max={np.abs(mu_g - mu_r.reshape(mu_g.shape)).max() / np.abs(mu_r).max():.2e} "
+          f"|dvar|={np.abs(var_g - var_r).max():.2e} {time.time() - t0:.1f}s")
+
+
+def test_dropin_resumes_from_reference_results_csv(tmp_path, engine):
+    """The drop-in resumes from a full reference results file (Bayesian7.py:268-286 semantics, optimizer.py
+    _ResultsTable.open): 3000 rows read back, one batch of 8 acquired and appended, and the final exact model (3008
+    points, Bayesian7's input / output transforms) equal to the oracle's fit of the same transformed data."""
+    from bayesianoptimizer_amd.optimizer import BayesianOptimizer, GPConfig
+    from tests.oracle_engine import to_oracle_params
+    from tests.stubs import BOUNDS as SB, StubSimulator
+
+    X, Yraw, _ = load("r3000")
+    out = tmp_path / "resume"
+    out.mkdir()
+    cols = ["n", "eta", "sigma_y", "width", "height"] + [f"x_{i:02d}" for i in range(1, 9)]
+    with open(out / "optimization_results.csv", "w") as fh:
+        fh.write(",".join(cols) + "\n")
+        for row in np.concatenate([X, Yraw], 1):
+            fh.write(",".join("%.16f" % v for v in row) + "\n")
+    sim = StubSimulator()
+    cfg = GPConfig(fit_hyperparameters=False, incremental_updates=False, candidates_pool_size=4096, acq_batch_size=512)
+    opt = BayesianOptimizer(sim, SB, str(out), n_initial_points=0, n_batches=1, batch_size=8, resume=True,
+                            target_total=3008, engine=engine, gp_config=cfg, seed=11)
+    best_params, best_value = opt.optimize()
+    sim.cleanup()
+    data = np.loadtxt(out / "optimization_results.csv", delimiter=",", skiprows=1)
+    assert data.shape[0] == 3008
+    np.testing.assert_array_equal(data[:3000, :5], X)
+    opt.fit_gp_model()
+    gp = opt.gp_model
+    Xt, Yt = gp.train_X.cpu().numpy(), gp.train_Y.cpu().numpy()
+    assert Xt.shape == (3008, 5)
+    ost = O.fit(Xt, Yt, to_oracle_params(gp.params.replace(jitter=gp.jitter_used), 5))
+    a = gp.state.alpha[:3008].cpu().numpy()
+    ar = ost.alpha.reshape(a.shape)
+    assert np.abs(a - ar).max() <= 1e-8 * np.abs(ar).max()
+    assert np.isfinite(best_value)

@@ -138,7 +138,9 @@ def test_log_standardize_inputs_matches_bayesian7_definition():
     np.testing.assert_allclose(Xs, (L - L.mean(0)) / L.std(0, ddof=1), rtol=1e-13)
 
 
-FIXTURES = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+# oracle-output fixtures (the results_* / validation_* files are reference INPUTS, tests/test_gpu_realdata.py)
+FIXTURES = sorted(f for f in glob.glob(os.path.join(GOLDEN, "*.npz"))
+                  if not os.path.basename(f).startswith(("results_", "validation_")))
 
 
 def _fixture_params(z):
@@ -159,6 +161,27 @@ def test_oracle_reproduces_golden(path):
     for acq, aid in [("ei", O.ACQ_EI), ("logei", O.ACQ_LOGEI), ("ucb", O.ACQ_UCB), ("variance", O.ACQ_VARIANCE)]:
         v, i, _ = O.acquire_argmax(st0, z["Xs"], aid, best_f=float(z["best_f"]), beta=float(z["beta"]))
         assert i == int(z[f"argmax_{acq}"])
+
+
+def test_reference_results_fixtures():
+    """The full-size reference data of tests/test_gpu_realdata.py: row counts of the five results files (one corrupt row
+    of optimization_results2.csv dropped), the 1550 duplicate X rows of optimization_results1009.csv, the validation
+    rows, and the oracle's jitter choice on the duplicate file's head (noise-free: fails at jitter 0, taken at 1e-4)."""
+    rows = {"r3000": (3000, 2), "r3901": (3901, 0), "r4235": (4235, 7), "r5000": (5000, 0), "r7740": (7740, 1550)}
+    for tag, (n, dup) in rows.items():
+        z = np.load(os.path.join(GOLDEN, f"results_{tag}.npz"))
+        assert z["X"].shape == (n, 5) and z["Y"].shape == (n, 8) and int(z["duplicate_rows"]) == dup, tag
+        assert np.isfinite(z["X"]).all() and np.isfinite(z["Y"]).all() and (z["Y"] > 0).all()
+    assert list(np.load(os.path.join(GOLDEN, "results_r5000.npz"))["dropped"]) == [2384]
+    assert np.load(os.path.join(GOLDEN, "validation_2048.npz"))["X"].shape == (2048, 5)
+    assert O.psd_safe_jitters() == [0.0, 1e-4, 1e-3, 1e-2, 1e-1, 1.0]
+    z = np.load(os.path.join(GOLDEN, "results_r7740.npz"))
+    lo, hi = np.array([0.3, 0.001, 0.001, 2.0, 2.0]), np.array([1.0, 300.0, 400.0, 7.0, 7.0])
+    Xu = (z["X"][:400] - lo) / (hi - lo)
+    p = O.KernelParams(O.SCALE_LINEAR_MATERN52, np.full(5, 0.4), outputscale=1.5, noise=0.0,
+                       linear_variance=np.linspace(0.05, 0.45, 5))
+    st, jit, failed = O.fit_with_jitter(Xu, np.log(z["Y"][:400]), p)
+    assert jit == 1e-4 and len(failed) == 1
 
 
 def test_golden_fixtures_present():
