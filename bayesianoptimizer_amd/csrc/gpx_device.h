@@ -212,6 +212,35 @@ struct MfmaTile {
     }
   }
 
+  // The same k-tile with the MFMAs in row-block-major order (for i: for k-substep: for j): every accumulator still sees
+  // its k values in ascending order (same bits), but the row block i = 0 needs only its own accumulators, so when acc is
+  // seeded by loads issued in i order the first MFMAs wait for the first quarter of the seeds instead of all of them.
+  __device__ __forceinline__ void compute_rows(const double* sA, const double* sB) {
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int wm0 = (w >> 1) * (TM / 2);
+    const int wn0 = (w & 1) * (TN / 2);
+    const int kr = lane >> 4, cl = lane & 15;
+    double b[BK / 4][WN];
+#pragma unroll
+    for (int s = 0; s < BK / 4; ++s) {
+      const int row = 4 * s + kr;
+      const int xb = B_KMAJOR ? 0 : (row & 14);
+#pragma unroll
+      for (int j = 0; j < WN; ++j) b[s][j] = sB[row * PB + ((wn0 + 16 * j + cl) ^ xb)];
+    }
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int s = 0; s < BK / 4; ++s) {
+        const int row = 4 * s + kr;
+        const int xa = A_KMAJOR ? 0 : (row & 14);
+        const double a = sA[row * PA + ((wm0 + 16 * i + cl) ^ xa)];
+#pragma unroll
+        for (int j = 0; j < WN; ++j) acc[i][j] = mfma16x16x4(a, b[s][j], acc[i][j]);
+      }
+  }
+
   // acc = -C (C: the TM x TN tile at Cg, row-major, leading dimension ldc): every load issued at once, so a following
   // run_acc(...) leaves acc = A B - C with no load round trip after the k loop (the caller stores -acc).
   __device__ __forceinline__ void load_neg_c(const double* __restrict__ Cg, int64_t ldc) {
@@ -241,7 +270,8 @@ struct MfmaTile {
 
   // run_acc with after_first() called once the first k-tile's global loads are issued (e.g. loads that seed acc: issued
   // behind the staging loads, so the first LDS store does not wait for them; kend > kbeg).
-  template <typename F>
+  // ROWS_FIRST: the first k-tile's MFMAs in row-block-major order (compute_rows), for seeds loaded by after_first.
+  template <bool ROWS_FIRST = false, typename F>
   __device__ __forceinline__ void run_acc_after(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
                                                 int64_t ldb, int kbeg, int kend, double* smem, F&& after_first) {
     if (kend <= kbeg) return;
@@ -251,6 +281,17 @@ struct MfmaTile {
     after_first();
     store_lds(cur, cur + BK * PA);
     __syncthreads();
+    if constexpr (ROWS_FIRST) {
+      const bool more = kbeg + BK < kend;
+      if (more) load_regs(A, lda, B, ldb, kbeg + BK);
+      compute_rows(cur, cur + BK * PA);
+      if (more) store_lds(nxt, nxt + BK * PA);
+      __syncthreads();
+      double* t = cur;
+      cur = nxt;
+      nxt = t;
+      kbeg += BK;
+    }
     for (int k0 = kbeg; k0 < kend; k0 += BK) {
       const bool more = (k0 + BK) < kend;
       if (more) load_regs(A, lda, B, ldb, k0 + BK);

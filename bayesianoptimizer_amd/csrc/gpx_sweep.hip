@@ -16,6 +16,7 @@
 // launch_argmax_final reduces the records of the whole sweep in one workgroup.
 #include "gpx_internal.h"
 #include "gpx_device.h"
+#include "gpx_trmm_asm.h"
 #include <cstdlib>
 
 namespace gpx {
@@ -272,7 +273,8 @@ __global__ void __launch_bounds__(WG) kstar_mfma_kernel(gpx_kernel_params p, int
 
 // ---- 2. triangular product + column sums of squares ------------------------------------------------------
 constexpr int TT = 128;  // trmm tile (rows of V x candidates)
-using TrmmTile = MfmaTile<TT, TT, 16, true, true>;
+using TrmmTile = MfmaTile<TT, TT, 16, true, true>;  // its accumulator layout (row_of / col_of) and LDS size
+static_assert(TrmmTile::LDS_DOUBLES * 8 == trmm_asm::LDS_BYTES, "hand-placed tile uses MfmaTile's LDS image");
 
 // kfull = 0: W upper triangular (k < (I+1)*128); kfull = 1: W is a full npad x npad matrix (the SVGP's
 // W2 = L^{-T} S term, gpx_svgp.hip), k over all nI row tiles.
@@ -296,8 +298,10 @@ __global__ void __launch_bounds__(WG) trmm_sumsq_kernel(const double* __restrict
   }
   const double* Ab = W + (int64_t)I * TT;            // A(m=i,k) = W[k][I*128 + i]
   const double* Bb = kstar + (int64_t)cb * TT;       // B(k,n=c) = K*[k][cb*128 + c]
-  TrmmTile tile;
-  tile.run(Ab, ldw, Bb, C, 0, (kfull ? nI : I + 1) * TT, smem);
+  // the k loop with a hand-placed instruction stream (gpx_trmm_asm.h; same MFMA sequence per accumulator as
+  // MfmaTile::run, so the same bits); for the triangular W, the waves of rows 0-63 skip the diagonal tile's zero half
+  trmm_asm::Tile tile;
+  tile.run(Ab, ldw, Bb, C, (kfull ? nI : I + 1) * (TT / 16), smem, !kfull);
   // column sums of squares over this wave's rows, then over the lanes holding the same column
   double s[TrmmTile::WN];
 #pragma unroll

@@ -284,7 +284,9 @@ def test_index_offset_and_combine(engine):
 
 
 # ---- golden fixtures ------------------------------------------------------------------------------------
-FIXTURES = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+# oracle-output fixtures (results_* / validation_* are reference inputs: tests/test_gpu_realdata.py)
+FIXTURES = sorted(f for f in glob.glob(os.path.join(GOLDEN, "*.npz"))
+                  if not os.path.basename(f).startswith(("results_", "validation_")))
 
 
 @pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(f) for f in FIXTURES])
