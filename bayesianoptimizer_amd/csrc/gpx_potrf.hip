@@ -598,29 +598,19 @@ __device__ __forceinline__ void trail_tile(int t, int T, int M, int xmap, int& I
 
 // acc = -C for an MfmaTile whose origin is C (row-major, leading dimension ld) through buffer loads: the lane's row / column
 // offset in one VGPR, each (i, r) row step wave-uniform (soffset) and each 16-column step an immediate, so the 64 seed loads
-// need no address registers.
-// 16-byte pairs (the inverse of store_block_pairs_sc1): the even lane of an adjacent pair loads columns (c, c + 1) of the
-// block's rows r = 0, 1, the odd lane the same columns of rows r = 2, 3, and one DPP swap of two values gives each lane its
-// own column of rows 0..3 - half the load instructions of one 8-byte load per accumulator element.
+// need no address registers.  (16-byte pair loads + a DPP lane swap, half the load instructions, spilled 9-12 VGPRs and
+// measured slower: update 1.684 vs 1.633 ms at n = 4096, profiles/r05_seed_ab.log.)
 template <typename T>
 __device__ __forceinline__ void load_neg_c_buf(T& tl, rsrc_t rc, int64_t ld) {
-  const bool even = (threadIdx.x & 1) == 0;
-  const int v0 = (int)(((int64_t)T::row_of(0, even ? 0 : 2) * ld + (T::col_of(0) & ~1)) * 8);
-  typedef double v2d __attribute__((ext_vector_type(2)));
+  const int v0 = (int)(((int64_t)T::row_of(0, 0) * ld + T::col_of(0)) * 8);
 #pragma unroll
   for (int i = 0; i < T::WM; ++i)
 #pragma unroll
-    for (int j = 0; j < T::WN; ++j) {
-      const int so0 = (int)((int64_t)(16 * i) * ld * 8), so1 = (int)((int64_t)(16 * i + 4) * ld * 8);
-      const v2d p = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rc, v0 + 128 * j, so0, 0));
-      const v2d q = __builtin_bit_cast(v2d, __builtin_amdgcn_raw_buffer_load_b128(rc, v0 + 128 * j, so1, 0));
-      // even lane: p = rows 0 (c, c+1), q = row 1 (4 rows down); odd lane: p = row 2, q = row 3
-      const double x0 = swap_adjacent_lanes(even ? p[1] : p[0]);
-      const double x1 = swap_adjacent_lanes(even ? q[1] : q[0]);
-      tl.acc[i][j][0] = -(even ? p[0] : x0);
-      tl.acc[i][j][1] = -(even ? q[0] : x1);
-      tl.acc[i][j][2] = -(even ? x0 : p[1]);
-      tl.acc[i][j][3] = -(even ? x1 : q[1]);
+    for (int r = 0; r < 4; ++r) {
+      const int so = (int)((int64_t)(16 * i + 4 * r) * ld * 8);
+#pragma unroll
+      for (int j = 0; j < T::WN; ++j)
+        tl.acc[i][j][r] = -__builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rc, v0 + 128 * j, so, 0));
     }
 }
 
