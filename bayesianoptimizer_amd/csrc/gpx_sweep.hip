@@ -282,13 +282,20 @@ __global__ void __launch_bounds__(WG) trmm_sumsq_kernel(const double* __restrict
                                                         const double* __restrict__ kstar, int64_t C, int nI, int ncb,
                                                         double* __restrict__ ss_part, int kfull) {
   __shared__ __attribute__((aligned(16))) double smem[TrmmTile::LDS_DOUBLES];
-  // Heaviest row tiles first.  XCD-aware when the candidate tiles split evenly over the 8 XCDs: workgroups
-  // b, b+8, ... share an XCD (dispatch is round-robin; speed only, never correctness), so XCD x gets the
-  // candidate tiles cb = x (mod 8) and walks them row tile by row tile: its ~64 resident workgroups share
-  // 8 W panels and 8 K* panels through one L2.
+  // Candidate tiles in groups of G = 64 (every row tile of a group, heaviest first, before the next group), and inside a
+  // group XCD-aware: workgroups b, b+8, ... share an XCD (dispatch is round-robin; speed only, never correctness), so
+  // XCD x gets the group's candidate tiles cb = x (mod 8) and walks them row tile by row tile.  Groups keep the K*
+  // panels the resident workgroups read to a quarter of the chunk at n = 4096: 7.65 vs 8.03 ms per launch (tools/
+  // trmm_asm_bench.hip A4 vs A2, profiles/r05_trmm_asm_groups.log; groups of 16 / 32 / 128: 8.17 / 7.91 / 7.82 ms).
   const int b = blockIdx.x;
   int I, cb;
-  if ((ncb & 7) == 0) {
+  constexpr int G = 64;
+  if ((ncb % G) == 0) {
+    const int g = b / (nI * G), bb = b % (nI * G);
+    const int x = bb & 7, l = bb >> 3;
+    I = nI - 1 - l / (G / 8);
+    cb = g * G + 8 * (l % (G / 8)) + x;
+  } else if ((ncb & 7) == 0) {
     const int x = b & 7, l = b >> 3, per = ncb >> 3;
     I = nI - 1 - l / per;
     cb = 8 * (l % per) + x;

@@ -44,9 +44,24 @@ __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
 trmm_v(const double* __restrict__ W, int64_t ldw, const double* __restrict__ kstar, int64_t C, int nI, int ncb,
        double* __restrict__ ss_part) {
   __shared__ __attribute__((aligned(16))) double smem[LDS_BYTES / 8];
-  const int b = blockIdx.x;
-  const int x = b & 7, l = b >> 3, per = ncb >> 3;
-  const int I = nI - 1 - l / per, cb = 8 * (l % per) + x;
+  int I, cb;
+  if constexpr (S >= 3 && S != 5) {
+    // candidate tiles in groups of G (all row tiles of a group, heaviest first, before the next group): the K* working
+    // set of the resident workgroups is G panels instead of all of them
+    constexpr int G = S == 3 ? 32 : S == 4 ? 64 : S == 6 ? 16 : S == 7 ? 128 : S == 8 ? 64 : 48;
+    const int g = blockIdx.x / (nI * G), bb = blockIdx.x % (nI * G);
+    const int x = bb & 7, l = bb >> 3, per = G >> 3;
+    I = nI - 1 - l / per;
+    cb = g * G + 8 * (l % per) + x;
+  } else {
+    const int b = blockIdx.x;
+    const int x = b & 7, l = b >> 3, per = ncb >> 3;
+    I = nI - 1 - l / per;
+    cb = 8 * (l % per) + x;
+  }
+  if constexpr (S == 5 || S == 8) {
+    if ((blockIdx.x >> 3) & 1) __builtin_amdgcn_s_setprio(1);
+  }
   const double* Ab = W + (int64_t)I * TT;
   const double* Bb = kstar + (int64_t)cb * TT;
   d4 accv[4][4];
@@ -59,7 +74,7 @@ trmm_v(const double* __restrict__ W, int64_t ldw, const double* __restrict__ kst
       for (int j = 0; j < 4; ++j) accv[i][j] = tile.acc[i][j];
   } else {
     gpx::trmm_asm::Tile tile;
-    tile.run(Ab, ldw, Bb, C, (I + 1) * TT / 16, smem, S == 2);
+    tile.run(Ab, ldw, Bb, C, (I + 1) * TT / 16, smem, S >= 2);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -94,7 +109,7 @@ trmm_v(const double* __restrict__ W, int64_t ldw, const double* __restrict__ kst
 }
 
 int main(int argc, char** argv) {
-  const int n = argc > 1 ? atoi(argv[1]) : 4096, C = 32768, nI = n / TT, ncb = C / TT;
+  const int n = argc > 1 ? atoi(argv[1]) : 4096, C = argc > 2 ? atoi(argv[2]) : 32768, nI = n / TT, ncb = C / TT;
   double *W, *K, *ss0, *ss1;
   CK(hipMalloc(&W, (size_t)n * n * 8));
   CK(hipMalloc(&K, (size_t)n * C * 8));
@@ -110,14 +125,22 @@ int main(int argc, char** argv) {
     for (auto& v : g) v = rand() / (double)RAND_MAX - 0.5;
     CK(hipMemcpy(K, g.data(), g.size() * 8, hipMemcpyHostToDevice));
   }
-  const char* names[] = {"S0 shipped", "A1 hand-placed", "A2 + diag skip"};
-  constexpr int NV = 3;
+  const char* names[] = {"S0 shipped", "A1 hand-placed", "A2 + diag skip", "A3 A2 + cb groups of 32",
+                         "A4 A2 + cb groups of 64", "A5 A2 + setprio half", "A6 A2 + groups of 16",
+                         "A7 A2 + groups of 128", "A8 A4 + setprio half"};
+  constexpr int NV = 9;
   auto run = [&](int v, double* out) {
     const dim3 g(ncb * nI);
     switch (v) {
       case 0: trmm_v<0><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
       case 1: trmm_v<1><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
-      default: trmm_v<2><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      case 2: trmm_v<2><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      case 3: trmm_v<3><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      case 4: trmm_v<4><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      case 5: trmm_v<5><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      case 6: trmm_v<6><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      case 7: trmm_v<7><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
+      default: trmm_v<8><<<g, WG>>>(W, n, K, C, nI, ncb, out); break;
     }
   };
   hipEvent_t e0, e1;
