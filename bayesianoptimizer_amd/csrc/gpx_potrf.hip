@@ -30,6 +30,7 @@
 #include "gpx_internal.h"
 #include "gpx_device.h"
 #include "gpx_chol64.h"
+#include "gpx_trmm_asm.h"
 
 // Optional timestamp hooks for tools/potrf_steps_probe.hip (compiled out in the library).
 #ifndef GPX_PANEL_STAMP
@@ -622,28 +623,56 @@ __device__ __forceinline__ void load_neg_c_buf(T& tl, rsrc_t rc, int64_t ld) {
 // round(C - ab) = -round(-C + ab)) or by a lookahead tile.  The factor, z and alpha are therefore bit-identical under every
 // schedule, batch size and GPX_OPT_POTRF_* option (tests/test_gpu_parity.py).  (Round 4 subtracted a from-zero product in
 // the epilogue, C - sum, whose rounding depended on how many columns a flush grouped.)
+// The 128 x 128 tiles run the hand-placed k loop of gpx_trmm_asm.h (both operands row-major: L panels), seeded with +C and
+// subtracting through the MFMA's A negation (the panel pre-update's form); the 128 x 64 halves keep MfmaTile, seeded with
+// -C and stored negated.  Both give every element the same MFMA chain, so the same bits.
 template <int TN>
 __device__ __forceinline__ void trailing_tile_at(double* __restrict__ A, int64_t lda, int c, int k0, int cfirst, int r0,
                                                  int q0, double* lds) {
   const double* Li = A + (int64_t)r0 * NB * lda + (int64_t)k0 * NB;
   const double* Lj = A + (int64_t)q0 * NB * lda + (int64_t)k0 * NB;
   double* C = A + (int64_t)r0 * NB * lda + (int64_t)q0 * NB;
-  using TileT = MfmaTile<2 * NB, TN, 16, false, false>;
-  TileT tl;
+  using TileT = MfmaTile<2 * NB, TN, 16, false, false>;  // (the accumulator layout of both forms)
   const rsrc_t rc = buf_rsrc(C);
-  tl.template run_acc_after<true>(Li, lda, Lj, lda, 0, (c - k0) * NB, lds, [&] { load_neg_c_buf(tl, rc, lda); });
+  d4 acc[TileT::WM][TileT::WN];
+  if constexpr (TN == 2 * NB) {
+    trmm_asm::TileT<false, false, true> tl;
+    tl.template run_after<false, false, TileT::WM * TileT::WN * 4>(
+        Li, lda, Lj, lda, (c - k0) * (NB / 16), lds, [&] {
+          const int v0 = (int)(((int64_t)TileT::row_of(0, 0) * lda + TileT::col_of(0)) * 8);
+#pragma unroll
+          for (int i = 0; i < TileT::WM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int so = (int)((int64_t)(16 * i + 4 * r) * lda * 8);
+#pragma unroll
+              for (int j = 0; j < TileT::WN; ++j)
+                tl.acc[i][j][r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rc, v0 + 128 * j, so, 0));
+            }
+        });
+#pragma unroll
+    for (int i = 0; i < TileT::WM; ++i)
+#pragma unroll
+      for (int j = 0; j < TileT::WN; ++j) acc[i][j] = tl.acc[i][j];
+  } else {
+    TileT tl;
+    tl.template run_acc_after<true>(Li, lda, Lj, lda, 0, (c - k0) * NB, lds, [&] { load_neg_c_buf(tl, rc, lda); });
+#pragma unroll
+    for (int i = 0; i < TileT::WM; ++i)
+#pragma unroll
+      for (int j = 0; j < TileT::WN; ++j) acc[i][j] = -tl.acc[i][j];
+  }
 #pragma unroll
   for (int i = 0; i < TileT::WM; ++i) {
-    // write-through 16-byte pairs of -acc; a 16-column pair never straddles a 64-block, and rows r = 0, 1 (even lanes) or
-    // 2, 3 (odd lanes) of one lane lie in one 64-row block
+    // write-through 16-byte pairs; a 16-column pair never straddles a 64-block, and rows r = 0, 1 (even lanes) or 2, 3
+    // (odd lanes) of one lane lie in one 64-row block
 #pragma unroll
     for (int j = 0; j < TileT::WN; ++j) {
       const int cb = q0 + (TileT::col_of(j) >> 6);
       const bool colok = cb >= cfirst;
       const bool k01 = colok && r0 + (TileT::row_of(i, 0) >> 6) >= cb;
       const bool k23 = colok && r0 + (TileT::row_of(i, 2) >> 6) >= cb;
-      const d4 v = -tl.acc[i][j];
-      store_block_pairs_sc1<TileT>(rc, lda, i, j, v, k01, k23);
+      store_block_pairs_sc1<TileT>(rc, lda, i, j, acc[i][j], k01, k23);
     }
   }
 }

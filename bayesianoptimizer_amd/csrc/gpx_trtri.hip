@@ -11,6 +11,7 @@
 //   launches in total.  Works for any even number of 64-blocks (the last group may be partial).
 #include "gpx_internal.h"
 #include "gpx_device.h"
+#include "gpx_trmm_asm.h"
 
 namespace gpx {
 
@@ -80,15 +81,33 @@ __global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ 
   auto tile_at = [&](int rb, int cb) {
     const double* Ab = L + off2 * ldl + off1 + rb * TS;  // A(m=r,k=q) = L[off2+q][off1+r]
     const double* Bb = W + off2 * ldw + off2 + cb * TS;  // B(k=q,n=c) = W[off2+q][off2+c]
-    Tile tile;
-    tile.run(Ab, ldl, Bb, ldw, 0, (cb + 1) * TS, smem);
+    d4 acc[Tile::WM][Tile::WN];
+    if constexpr (TS == 128) {
+      // the hand-placed k loop (gpx_trmm_asm.h, same bits as MfmaTile::run); B = W22's diagonal 128-tile is zero in its
+      // last 64 k-rows for the left 64 columns, so those waves skip the last 4 k-tiles' MFMAs
+      trmm_asm::TileT<true, true> tile;
+      tile.zero();
+      const bool skip = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) & 1) == 0;
+      tile.template run<false, true>(Ab, ldl, Bb, ldw, (cb + 1) * (TS / 16), smem, false, skip);
+#pragma unroll
+      for (int i = 0; i < Tile::WM; ++i)
+#pragma unroll
+        for (int j = 0; j < Tile::WN; ++j) acc[i][j] = tile.acc[i][j];
+    } else {
+      Tile tile;
+      tile.run(Ab, ldl, Bb, ldw, 0, (cb + 1) * TS, smem);
+#pragma unroll
+      for (int i = 0; i < Tile::WM; ++i)
+#pragma unroll
+        for (int j = 0; j < Tile::WN; ++j) acc[i][j] = tile.acc[i][j];
+    }
 #pragma unroll
     for (int i = 0; i < Tile::WM; ++i)
 #pragma unroll
       for (int j = 0; j < Tile::WN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          Tp[(int64_t)(rb * TS + Tile::row_of(i, r)) * b2 + cb * TS + Tile::col_of(j)] = tile.acc[i][j][r];
+          Tp[(int64_t)(rb * TS + Tile::row_of(i, r)) * b2 + cb * TS + Tile::col_of(j)] = acc[i][j][r];
   };
   if constexpr (PAIRED) {
     const int rb = blockIdx.y, x = blockIdx.x;
@@ -123,15 +142,34 @@ __global__ void __launch_bounds__(WG) trtri_w_kernel(double* __restrict__ W, int
   auto tile_at = [&](int rb, int cb) {
     const double* Bb = T + (int64_t)p * b1 * b1 + cb * TS;  // B(k=q,n=c) = T[q][c], row length b2
     const double* Ab = W + (off1 + rb * TS) * ldw + off1;   // A(m=r,k=q) = W[off1+r][off1+q]
-    Tile tile;
-    tile.run(Ab, ldw, Bb, b2, rb * TS, b1, smem);
+    d4 acc[Tile::WM][Tile::WN];
+    if constexpr (TS == 128) {
+      // the hand-placed k loop from k = rb * TS (A row-major: W11 read along its rows); A = W11's diagonal 128-tile is
+      // zero in its first 64 k-columns for the lower 64 rows, so those waves skip the first 4 k-tiles' MFMAs
+      trmm_asm::TileT<false, true> tile;
+      tile.zero();
+      const bool skip = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7) == 1;
+      tile.template run<true, false>(Ab + rb * TS, ldw, Bb + (int64_t)rb * TS * b2, b2, (b1 - rb * TS) / 16, smem, skip,
+                                     false);
+#pragma unroll
+      for (int i = 0; i < Tile::WM; ++i)
+#pragma unroll
+        for (int j = 0; j < Tile::WN; ++j) acc[i][j] = tile.acc[i][j];
+    } else {
+      Tile tile;
+      tile.run(Ab, ldw, Bb, b2, rb * TS, b1, smem);
+#pragma unroll
+      for (int i = 0; i < Tile::WM; ++i)
+#pragma unroll
+        for (int j = 0; j < Tile::WN; ++j) acc[i][j] = tile.acc[i][j];
+    }
     double* Wo = W + (off1 + rb * TS) * ldw + off2 + cb * TS;
 #pragma unroll
     for (int i = 0; i < Tile::WM; ++i)
 #pragma unroll
       for (int j = 0; j < Tile::WN; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Wo[(int64_t)Tile::row_of(i, r) * ldw + Tile::col_of(j)] = -tile.acc[i][j][r];
+        for (int r = 0; r < 4; ++r) Wo[(int64_t)Tile::row_of(i, r) * ldw + Tile::col_of(j)] = -acc[i][j][r];
   };
   if constexpr (PAIRED) {
     const int cb = blockIdx.x, y = blockIdx.y;
