@@ -38,6 +38,7 @@ struct Context {
   int gram_split = 0;      // 0 by size, else workgroups per Gram tile
   int potrf_lazy = 0;      // multi-launch flush interval, 0 by size
   int potrf_mode = -1;     // multi-launch panel mode, -1 by size
+  int potrf_switch = -1;   // launch at which a single fit switches schedule (gpx_potrf.hip potrf_switch), -1 by size
 };
 
 // Scoped device switch of one C ABI call: makes the handle's device current and restores the caller's current device

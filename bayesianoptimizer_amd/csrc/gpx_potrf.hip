@@ -925,13 +925,30 @@ static int potrf_mode(const Context* ctx, int nblk, int batch) {
 // launches' panel chain is the shorter one (profiles/r04_potrf_eager_tail_ab.log: n = 8192 5.832 -> 5.720 ms with the
 // last 32, 5.811 -> 5.748 with 24, 5.796 -> 5.731 with 48; n = 16384 29.865 -> 29.715 with 32).
 constexpr int kEagerTail = 32;
+constexpr int kSwitchLazy = 4;  // the flush interval before the switch (the switch launch follows a flush launch)
+// flush interval of the launches before the switch: mode 0 (eager after it) kSwitchLazy or GPX_OPT_POTRF_LAZY when the
+// switch is set by option; mode 1 (lookahead before it) the schedule's own interval g
+static int early_lazy(const Context* ctx, int mode, int g) {
+  if (mode != 0) return g;
+  return (ctx->potrf_switch >= 0 && ctx->potrf_lazy > 0) ? ctx->potrf_lazy : kSwitchLazy;
+}
 static int potrf_switch(const Context* ctx, int nblk, int batch, int mode, int g) {
-  if (ctx->potrf_mode >= 0 || ctx->potrf_lazy > 0 || batch != 1) return 0;
+  if (ctx->potrf_switch >= 0) {  // GPX_OPT_POTRF_SWITCH, rounded down to the launch after a flush of the early schedule
+    const int ge = early_lazy(ctx, mode, g);  // (the fold needs the eager panels to apply one column)
+    const int sw = ctx->potrf_switch;
+    return sw <= 1 ? sw : ((sw - 1) / ge) * ge + 1;
+  }
+  if (ctx->potrf_mode >= 0 || ctx->potrf_lazy > 0) return 0;
+  if (batch != 1) {
+    // batches on the lookahead schedule finish on the eager one for their last ~16 block columns (B = 4, n = 4096:
+    // 3.195 -> 3.149 ms with the switch at 49, 3.153 at 37, 3.219 at 25; profiles/r05_potrf_schedules.log)
+    if (!batched_lookahead(nblk, batch)) return 0;
+    return ((nblk - 16 - 1) / g) * g + 1;
+  }
   if (mode == 0) return nblk == 64 ? 9 : 0;
   if (nblk - kEagerTail < g + 1) return 0;
   return ((nblk - kEagerTail - 1) / g) * g + 1;
 }
-constexpr int kSwitchLazy = 4;  // the flush interval before the switch (the switch launch follows a flush launch)
 
 // The plan of every launch c < cend (flush launches: c >= 1 and at least one interval after the previous flush);
 // launches c < sw (potrf_switch) run the lookahead schedule, the rest the eager one with a flush every launch.
@@ -939,7 +956,7 @@ template <typename F>
 static void for_each_step(const Context* ctx, int nblk, int batch, int mode, int cend, int slots, F&& f) {
   const int g = potrf_lazy(ctx, nblk, batch);
   const int sw = potrf_switch(ctx, nblk, batch, mode, g);
-  const int ge = mode == 0 ? kSwitchLazy : g;
+  const int ge = early_lazy(ctx, mode, g);
   int last = 0;
   for (int c = 0; c < cend; ++c) {
     const bool early = c < sw;
@@ -991,7 +1008,9 @@ hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* 
   if (z_done) *z_done = false;
   PotrfFwd f;
   // the fold needs panels that apply exactly one pending column per launch (eager or lookahead schedules)
-  if (fr && fr->Y && fr->buf && (potrf_mode(ctx, nblk, bt.count) == 1 || potrf_lazy(ctx, nblk, bt.count) == 1)) {
+  // (lookahead launches always do; eager ones when they flush every launch: g = 1, or after a switch)
+  const int fmode = potrf_mode(ctx, nblk, bt.count), fg = potrf_lazy(ctx, nblk, bt.count);
+  if (fr && fr->Y && fr->buf && (fmode == 1 || fg == 1 || potrf_switch(ctx, nblk, bt.count, fmode, fg) > 0)) {
     const int64_t nr = rhs_row(fr->nrhs);
     f.Y = fr->Y;
     f.ldy = fr->ldy;

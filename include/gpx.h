@@ -144,7 +144,10 @@ size_t gpx_acq_params_size(void);
  *  GPX_OPT_SWEEP_FUSED     1 (default) the fused small-n sweep where it applies (padded n <= 256), 0 the K* + trmm path
  *  GPX_OPT_GRAM_SPLIT      0 by size (default), else 1, 2 or 4 workgroups per 64x64 Gram tile
  *  GPX_OPT_POTRF_LAZY      multi-launch schedule: 0 by size and batch (default), else flush the trailing update every g columns
- *  GPX_OPT_POTRF_MODE      multi-launch schedule: -1 by size and batch (default), 0 eager panels, 1 lookahead panels */
+ *  GPX_OPT_POTRF_MODE      multi-launch schedule: -1 by size and batch (default), 0 eager panels, 1 lookahead panels
+ *  GPX_OPT_POTRF_SWITCH    multi-launch schedule: -1 by size and batch (default), 0 no switch, k > 0: launches < k on
+ *                          the lookahead schedule (flush every potrf_lazy, default 4 / by size), the rest eager (rounded
+ *                          down to the launch after a flush) */
 enum {
   GPX_OPT_RESERVED_0 = 0,
   GPX_OPT_SPIN_LIMIT = 1,
@@ -152,7 +155,8 @@ enum {
   GPX_OPT_GRAM_SPLIT = 3,
   GPX_OPT_POTRF_LAZY = 4,
   GPX_OPT_POTRF_MODE = 5,
-  GPX_OPT_COUNT = 6
+  GPX_OPT_POTRF_SWITCH = 6,
+  GPX_OPT_COUNT = 7
 };
 gpx_status gpx_set_option(gpx_handle h, int32_t option, int64_t value);
 gpx_status gpx_get_option(gpx_handle h, int32_t option, int64_t* value_host);

@@ -95,14 +95,14 @@ def test_batched_timeout_names_the_problem(engine):
 
 def test_options_roundtrip_and_validation(engine):
     for name, value in (("spin_limit", 12345), ("sweep_fused", 0), ("gram_split", 2),
-                        ("potrf_lazy", 3), ("potrf_mode", 1)):
+                        ("potrf_lazy", 3), ("potrf_mode", 1), ("potrf_switch", 13)):
         old = engine.get_option(name)
         engine.set_option(name, value)
         assert engine.get_option(name) == value
         engine.set_option(name, old)
         assert engine.get_option(name) == old
     for name, bad in (("spin_limit", -1), ("sweep_fused", 2), ("gram_split", 3),
-                      ("potrf_lazy", 17), ("potrf_mode", 2)):
+                      ("potrf_lazy", 17), ("potrf_mode", 2), ("potrf_switch", -2)):
         with pytest.raises(GPXError) as e:
             engine.set_option(name, bad)
         assert e.value.status == _capi.GPX_INVALID_ARG
@@ -129,7 +129,8 @@ def test_options_from_environment_at_create(capfd):
     assert e2.get_option("gram_split") == 0
 
 
-SCHEDULES = ((0, 1), (1, 1), (1, 4), (1, 6), (1, 8))  # (potrf_mode, potrf_lazy): eager, lookahead with flushes every g
+# (potrf_mode, potrf_lazy, potrf_switch): eager, lookahead with flushes every g, hybrids switching at launch 5 / 17
+SCHEDULES = ((0, 1, -1), (1, 1, -1), (1, 4, -1), (1, 6, -1), (1, 8, -1), (-1, 2, 5), (-1, 4, 17))
 
 
 @pytest.mark.parametrize("n", [4096, 8320])
@@ -145,16 +146,18 @@ def test_fit_bits_identical_across_schedules_and_batches(engine, n):
     ref = engine.fit(t(X), t(y), kp)
     L0, a0 = torch.tril(ref.L).clone(), ref.alpha.clone()
     del ref
-    for mode, lazy in SCHEDULES:
+    for mode, lazy, sw in SCHEDULES:
         engine.set_option("potrf_mode", mode)
         engine.set_option("potrf_lazy", lazy)
+        engine.set_option("potrf_switch", sw)
         try:
             st = engine.fit(t(X), t(y), kp)
         finally:
             engine.set_option("potrf_mode", -1)
             engine.set_option("potrf_lazy", 0)
-        assert torch.equal(torch.tril(st.L), L0), (mode, lazy)
-        assert torch.equal(st.alpha, a0), (mode, lazy)
+            engine.set_option("potrf_switch", -1)
+        assert torch.equal(torch.tril(st.L), L0), (mode, lazy, sw)
+        assert torch.equal(st.alpha, a0), (mode, lazy, sw)
         del st
     for B in ((2, 4) if n == 4096 else (2,)):
         sts = engine.fit_batched(t(np.stack([X] * B)), t(np.stack([y] * B)), kp)
