@@ -1,0 +1,7 @@
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out/trace10
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/trace10 -o fit -- python3 $R/tools/fit_only.py --n 16384 --kernel matern52 --reps 2 > $R/gpurun_out/trace10.log 2>&1 || exit $?
+cd $R
+python3 tools/potrf_launches.py gpurun_out/trace10 8 > gpurun_out/r05_potrf_launches_16384.log 2>&1
