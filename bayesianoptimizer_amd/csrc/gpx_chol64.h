@@ -4,8 +4,11 @@
 // Register layout of a 16x16 block in a wave: lane = r + 16 g owns row r, columns 4g..4g+3.  At pivot j the pivot
 // A[j][j] is one lane's register (v_readlane, uniform); every lane applies the unscaled rank-1 update
 // A[r][c] -= A[r][j] A[j][c] / A[j][j] and the same row operation on X = L^{-1}, with the cross-lane operands moved
-// by DPP and gfx950 permlane swaps, so only the pivot's rsq sits between two consecutive pivots.  LDS tiles use a padded row
-// length LD64 (doubles).
+// by DPP and gfx950 permlane swaps, so only the pivot's rsq sits between two consecutive pivots.  Row j is final from
+// pivot j on (its multiplier is 0), so after the last pivot the registers hold the unscaled upper factor U (row j =
+// A^(j)[j][.], U[j][j] the pivot) and L = (U diag(1/sqrt(U[j][j])))^T needs no capture on the pivot chain: the panel
+// scales it only where L_cc is stored (round 5: the per-pivot column capture cost 484 of 3628 cycles per block,
+// profiles/r04_chol16_split.log).  LDS tiles use a padded row length LD64 (doubles).
 #pragma once
 #include <utility>
 #include "gpx_device.h"
@@ -37,9 +40,8 @@ __device__ __forceinline__ double pivot_rsq(double piv) {
 }
 
 struct Blk16 {
-  double a[4];  // A: trailing rows updated in place; a row becomes scratch once it has been pivoted
+  double a[4];  // A: trailing rows updated in place; row j is final (U) once pivot j has been applied
   double x[4];  // X = L^{-1} (the factorisation's row operations applied to I)
-  double l[4];  // L, captured column by column
 };
 
 // Lane J of every 16-lane row, broadcast to the whole row, as two v_mov_b32_dpp row_newbcast:J (no old value;
@@ -150,13 +152,11 @@ __device__ __forceinline__ void fmac_pipe_rest(double& a1, double& a2, double& a
 // J+1.  Same operations on the same values as chol16_pivot_fused (bit-identical L and X).
 template <int J>
 __device__ __forceinline__ void chol16_pivot_pipe(Blk16& b, int r, int g, int& fail, double& piv, double& arj) {
-  constexpr int GJ = J >> 2, QJ = J & 3;
   if (!(piv > 0.0) && fail < 0) fail = J;
   const double isq = pivot_rsq(piv);
   const double rinv = isq * isq;
   const double coef = (r > J) ? -arj * rinv : 0.0;
   const double coefx = (r == J) ? isq - 1.0 : coef;
-  if (g == GJ) b.l[QJ] = (r >= J) ? b.a[QJ] * isq : 0.0;
   if constexpr (J < 15) {
     constexpr int JN = J + 1, GN = JN >> 2, QN = JN & 3;
     fmac_pipe_first<J>(b.a[QN], coef);
@@ -176,23 +176,21 @@ __device__ __forceinline__ void chol16_pivots(Blk16& b, int r, int g, int& fail,
   (chol16_pivot_pipe<J>(b, r, g, fail, piv, arj), ...);
 }
 
-// Factor + invert a 16x16 SPD block held in registers (lane = r + 16 g: b.a[q] = A[r][4g + q]): L into b.l, L^{-1}
-// into b.x.  Returns the 0-based failing pivot inside the block, or -1 (uniform).
+// Factor + invert a 16x16 SPD block held in registers (lane = r + 16 g: b.a[q] = A[r][4g + q]): the unscaled upper
+// factor U into b.a (rows; below the diagonal: eliminated residue), L^{-1} into b.x.  Returns the 0-based failing pivot
+// inside the block, or -1 (uniform).
 __device__ __forceinline__ int chol16_regs(Blk16& b) {
   const int lane = threadIdx.x & 63;
   const int r = lane & 15, g = lane >> 4;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    b.x[q] = (r == 4 * g + q) ? 1.0 : 0.0;
-    b.l[q] = 0.0;
-  }
+  for (int q = 0; q < 4; ++q) b.x[q] = (r == 4 * g + q) ? 1.0 : 0.0;
   int fail = -1;
   chol16_pivots(b, r, g, fail, std::make_integer_sequence<int, 16>{});
   return fail;
 }
 
-// L (strict upper zeroed) into the LDS tile sA at (o, o), D = L^{-1} (lower, strict upper 0) into the 16x16 tile sD of
-// row length LDD.
+// U (unscaled upper factor, rows; only its upper triangle is meaningful) into the LDS tile sA at (o, o), D = L^{-1}
+// (lower, strict upper 0) into the 16x16 tile sD of row length LDD.
 template <int LDD>
 __device__ __forceinline__ void chol16_store(const Blk16& b, double* sA, double* sD, int o) {
   const int lane = threadIdx.x & 63;
@@ -200,13 +198,26 @@ __device__ __forceinline__ void chol16_store(const Blk16& b, double* sA, double*
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int c = 4 * g + q;
-    sA[(o + r) * LD64 + o + c] = b.l[q];
+    sA[(o + r) * LD64 + o + c] = b.a[q];
     sD[r * LDD + c] = (c <= r) ? b.x[q] : 0.0;
   }
 }
 
+// L_cc[r][c] (c <= r) of a factored 64x64 diagonal tile whose 16x16 diagonal blocks hold U (chol16_store) and whose
+// blocks below them hold L (the T step): the diagonal blocks give L[r][c] = U[c][r] / sqrt(U[c][c]) (the pivot_rsq of
+// the chain, recomputed from the same pivot: the same bits), isq: 64 doubles of scratch filled by l64_isq.
+__device__ __forceinline__ void l64_isq(const double* sA, double* isq) {
+  const int t = threadIdx.x;
+  if (t < 64) isq[t] = pivot_rsq(sA[t * LD64 + t]);
+}
+__device__ __forceinline__ double l64_at(const double* sA, const double* isq, int r, int c) {
+  if (c > r) return 0.0;
+  if ((c >> 4) == (r >> 4)) return sA[c * LD64 + r] * isq[c];
+  return sA[r * LD64 + c];
+}
+
 // Factor + invert the 16x16 SPD block at (o, o) of the LDS tile sA (both triangles present, symmetric) with one
-// wave: L back into sA, D = L^{-1} into sD (chol16_store).  Returns the failing pivot inside the block, or -1.
+// wave: U back into sA, D = L^{-1} into sD (chol16_store).  Returns the failing pivot inside the block, or -1.
 template <int LDD>
 __device__ __forceinline__ int chol16(double* sA, double* sD, int o) {
   const int lane = threadIdx.x & 63;

@@ -538,10 +538,10 @@ __device__ __forceinline__ void panel_role(double* __restrict__ A, int64_t lda, 
   if (!panel) {
     if (t == 0 && fail >= 0) atomicCAS(info, 0, c * NB + fail + 1);
     double* Lcc = Dinv + (int64_t)(nblk + c) * NB * NB;  // scratch copy, moved into A by potrf_dinv
-    for (int e = t; e < NB * NB; e += WG) {
-      const int r = e >> 6, cc = e & 63;
-      Lcc[e] = (cc <= r) ? sA[r * LD64 + cc] : 0.0;
-    }
+    double* isq = sDb;  // the D buffers are free after the last step
+    l64_isq(sA, isq);
+    __syncthreads();
+    for (int e = t; e < NB * NB; e += WG) Lcc[e] = l64_at(sA, isq, e >> 6, e & 63);
     if constexpr (NR > 0) {
       for (int e = t; e < NB * NR; e += WG) f.z[(int64_t)c * NB * NR + e] = sZall[e];
     }
