@@ -114,7 +114,7 @@ int main(int argc, char** argv) {
   for (int c = 0; c < nblk; ++c) {
     const unsigned long long* P = &pan[c * 16];
     const unsigned long long end = pe[c] > te[c] ? pe[c] : te[c];
-    if (c < 6 || c % 8 == 0 || c >= nblk - 3)
+    if (c < 6 || c % 8 == 0 || (c > 8 && c < 16) || (c > 96 && c < 104) || (c > 168 && c < 176) || c >= nblk - 3)
       printf("%3d %7.2f %8.2f %8.2f | %6.2f %5.2f %5.2f %5.2f %5.2f %5.2f %5.2f %5.2f\n", c, us(f[c]), us(pe[c]),
              te[c] ? us(te[c]) : -1.0, us(P[0]), (double)(P[1] - P[0]) / 100, (double)(P[2] - P[1]) / 100,
              (double)(P[3] - P[2]) / 100, (double)(P[4] - P[3]) / 100, (double)(P[5] - P[4]) / 100,
