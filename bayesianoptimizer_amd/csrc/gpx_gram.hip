@@ -109,7 +109,8 @@ __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, in
 // ||a||^2 + ||b||^2 - 2 a.b on centred, lengthscale-scaled inputs, clamped at 0, exactly 0 for a point with itself).
 // The difference form above spends ~2 d VALU ops and d LDS reads per element on the distance (16 + 8 at d = 8) beside
 // ~22 for exp; here a.b of a 16 x 16 block is DMAX/4 v_mfma_f64_16x16x4 and the element epilogue is r2 = max(na + nb -
-// 2 a.b, 0) and the covariance.  Centring: by the mean of the tile's (valid) row block, so a tile depends only on its
+// 2 a.b, 0) and the covariance.  Centring: by the first row of the tile's row block (round 5; the mean of its valid rows
+// before: 29.0 -> 27.7 us at n = 4096, profiles/r05_gram_ab.log), so a tile depends only on its
 // own rows and columns (an appended row block reproduces a refit bit for bit) and |a|, |b| stay O(spread / lengthscale);
 // the gap to the difference form is O(eps (|a|^2 + |b|^2)) per entry (bounded in tests/test_oracle.py).  The ARD linear
 // term of ScaleKernel(Linear + Matern) is a second MFMA dot (raw x_i v against raw x_j).
@@ -117,7 +118,8 @@ __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, in
 // v_mfma_f64_16x16x4 gives each lane rows (lane >> 4) + 4 r of column lane & 15 of a block, so a store instruction writes
 // four 128-byte row segments.  Measured and not kept (profiles/r04_gram128_ab.log, r04_gram_rowstore_ab.log): whole-row
 // 512-byte stores through a permlane transpose (as kstar_mfma_kernel does) 34.0 vs 28.9 us at n = 4096, and 128 x 128
-// tiles 33.5 vs 29.3 us (331 vs 365 us at n = 16384).
+// tiles 33.5 vs 29.3 us (331 vs 365 us at n = 16384); round 5, two rows of 256 B per store (column blocks paired by
+// v_permlane32_swap) 28.0 vs 27.7 us (profiles/r05_gram_ab.log).
 template <int DMAX, int KIND>
 __global__ void __launch_bounds__(WG) gram_mfma_kernel(gpx_kernel_params p, int n, int t0, const double* __restrict__ X,
                                                        int64_t ldx, double* __restrict__ K, int64_t ldk, int64_t sx,
@@ -135,37 +137,29 @@ __global__ void __launch_bounds__(WG) gram_mfma_kernel(gpx_kernel_params p, int 
   constexpr int KS = DMAX / 4;  // MFMA k-steps
   // a, b: centred scaled inputs (k >= d zero); ra: raw x_i * linear variance, rb: raw x_j; na, nb: squared norms
   __shared__ double sa[NB][DMAX + 1], sb[NB][DMAX + 1], ra[lin ? NB : 1][DMAX + 1], rb[lin ? NB : 1][DMAX + 1];
-  __shared__ double na[NB], nb[NB], cen[DMAX];
+  __shared__ double na[NB], nb[NB];
   int ti, tj;
   tri_decode(t0 + (int)blockIdx.x, ti, tj);
   const int i0 = ti * NB, j0 = tj * NB;
   const int d = p.d, t = threadIdx.x;
   const int nv = n - i0 < NB ? n - i0 : NB;  // valid rows of the row block (<= 0: all padding)
+  // centre: the row block's first row (any common shift is exact in real arithmetic; the first row keeps |a|, |b|
+  // within the block's spread as the mean does, without the mean's serial 64-row sum and two extra barriers)
   for (int e = t; e < NB * DMAX; e += WG) {
     const int r = e / DMAX, k = e % DMAX;
-    double xi = 0.0, xj = 0.0;
+    double xi = 0.0, xj = 0.0, x0 = 0.0;
     if (k < d) {
       if (i0 + r < n) xi = X[(int64_t)(i0 + r) * ldx + k];
       if (j0 + r < n) xj = X[(int64_t)(j0 + r) * ldx + k];
+      if (nv > 0) x0 = X[(int64_t)i0 * ldx + k];
     }
-    sa[r][k] = (k < d) ? xi / p.lengthscale[k] : 0.0;
-    sb[r][k] = (k < d) ? xj / p.lengthscale[k] : 0.0;
+    const double c0 = (k < d) ? x0 / p.lengthscale[k] : 0.0;
+    sa[r][k] = (k < d) ? xi / p.lengthscale[k] - c0 : 0.0;
+    sb[r][k] = (k < d) ? xj / p.lengthscale[k] - c0 : 0.0;
     if constexpr (lin) {
       ra[r][k] = (k < d) ? xi * p.linear_variance[k] : 0.0;
       rb[r][k] = xj;
     }
-  }
-  __syncthreads();
-  if (t < DMAX) {  // centre: mean of the valid rows of the row block, summed in row order
-    double s = 0.0;
-    for (int r = 0; r < nv; ++r) s += sa[r][t];
-    cen[t] = nv > 0 ? s / nv : 0.0;
-  }
-  __syncthreads();
-  for (int e = t; e < NB * DMAX; e += WG) {
-    const int r = e / DMAX, k = e % DMAX;
-    sa[r][k] -= cen[k];
-    sb[r][k] -= cen[k];
   }
   __syncthreads();
   if (t < 2 * NB) {
@@ -179,6 +173,15 @@ __global__ void __launch_bounds__(WG) gram_mfma_kernel(gpx_kernel_params p, int 
   __syncthreads();
   const int lane = t & 63, w = t >> 6, m = lane & 15, kq = lane >> 4;
   const double diag_add = p.noise + p.jitter;
+  auto element = [&](int rr, int c, double dot, double ldot) {  // K[i0 + rr][j0 + c]
+    const int gi = i0 + rr, gj = j0 + c;
+    double r2 = sqdist_expanded(na[rr], nb[c], dot);
+    if (gi == gj) r2 = 0.0;
+    double v = cov_from_r2(KIND, p.outputscale, r2, ldot);
+    if (gi == gj) v += diag_add;
+    if (gi >= n || gj >= n) v = (gi == gj) ? 1.0 : 0.0;  // identity padding
+    return v;
+  };
   // gridDim.z row slices (small fits): the slice's 16-row strips x 4 column blocks, dealt to the waves
   const int strips = 4 / gridDim.z, s0 = blockIdx.z * strips;
   for (int b = w; b < strips * 4; b += 4) {
@@ -189,17 +192,11 @@ __global__ void __launch_bounds__(WG) gram_mfma_kernel(gpx_kernel_params p, int 
       acc = mfma16x16x4(sa[rs + m][4 * k + kq], sb[cs + m][4 * k + kq], acc);
       if constexpr (lin) lac = mfma16x16x4(ra[rs + m][4 * k + kq], rb[cs + m][4 * k + kq], lac);
     }
-    const int c = cs + m, gj = j0 + c;
-    const double nbc = nb[c];
+    const int c = cs + m;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int rr = rs + kq + 4 * r, gi = i0 + rr;
-      double r2 = sqdist_expanded(na[rr], nbc, acc[r]);
-      if (gi == gj) r2 = 0.0;
-      double v = cov_from_r2(KIND, p.outputscale, r2, lin ? lac[r] : 0.0);
-      if (gi == gj) v += diag_add;
-      if (gi >= n || gj >= n) v = (gi == gj) ? 1.0 : 0.0;  // identity padding
-      K[(int64_t)gi * ldk + gj] = v;
+      const int rr = rs + kq + 4 * r;
+      K[(int64_t)(i0 + rr) * ldk + j0 + c] = element(rr, c, acc[r], lin ? lac[r] : 0.0);
     }
   }
 }
