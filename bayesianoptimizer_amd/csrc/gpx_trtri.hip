@@ -40,16 +40,23 @@ __global__ void __launch_bounds__(WG) trtri_diag_kernel(const double* __restrict
 // (tools/trtri_bench.hip, profiles/r04_trtri_order_bench.log; same tiles, bit-identical); the whole inverse
 // 25.7 -> 23.6 ms.  The 64-tile levels keep the paired order (PAIRED: a workgroup takes the k-ranges of tile pair
 // (x, nt - 1 - x), so every workgroup does the same work; the XCD order measured 0.72 vs 0.66 ms at n = 4096).
-// nH / nF: tile counts of a full group; tiles past a partial last group exit.
-__device__ __forceinline__ void trtri_order(int b, int nH, int nF, bool heavy_high, int& H, int& F) {
+// nH / nF: tile counts of a full group; tiles past a partial last group exit.  The groups of a level share one grid
+// dimension with the heavy index outermost (round 5): every group's heaviest tiles start first, instead of group
+// g + 1's heaviest tiles waiting behind group g's light ones (n = 16384, levels h = 32 / 64: 4 / 2 groups).
+__device__ __forceinline__ void trtri_order(int b, int nH, int nF, int groups, bool heavy_high, int& H, int& F,
+                                            int& g) {
   int q;
   if ((nF & 7) == 0) {
     const int l = b >> 3, per = nF >> 3;
-    q = l / per;
-    F = 8 * (l % per) + (b & 7);
+    q = l / (per * groups);
+    const int rem = l % (per * groups);
+    g = rem / per;
+    F = 8 * (rem % per) + (b & 7);
   } else {
-    q = b / nF;
-    F = b % nF;
+    q = b / (nF * groups);
+    const int rem = b % (nF * groups);
+    g = rem / nF;
+    F = rem % nF;
   }
   H = heavy_high ? nH - 1 - q : q;
 }
@@ -65,7 +72,13 @@ __global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ 
                                                      int64_t sw, int64_t st) {
   using Tile = MfmaTile<TS, TS, 16, true, true>;
   __shared__ __attribute__((aligned(16))) double smem[Tile::LDS_DOUBLES];
-  const int p = blockIdx.z % groups, prob = blockIdx.z / groups;
+  // PAIRED: group and problem in blockIdx.z; else the group is decoded from blockIdx.x (trtri_order), problem = z
+  int p = PAIRED ? (int)(blockIdx.z % groups) : 0, ocb = 0, orb = 0;
+  const int prob = PAIRED ? (int)(blockIdx.z / groups) : (int)blockIdx.z;
+  if constexpr (!PAIRED) {
+    const int h1 = h * NB / TS;
+    trtri_order(blockIdx.x, h1, h1, groups, true, ocb, orb, p);
+  }
   L += prob * sl;
   W += prob * sw;
   T += prob * st;
@@ -73,7 +86,7 @@ __global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ 
   const int nb2 = min(2 * h, nblk - s1) - h;
   if (nb2 <= 0) return;
   const int b1 = h * NB, b2 = nb2 * NB;
-  const int nt1 = b1 / TS, nt2 = b2 / TS;
+  const int nt2 = b2 / TS;
   const int64_t off1 = (int64_t)s1 * NB, off2 = (int64_t)s2 * NB;
   // T_p is b1 x b2 with row length b2; every group before the last is full (b2 = b1), so group p starts at
   // p*b1*b1 and the level's total sum_p b1*b2_p <= b1*(npad-b1) <= npad^2/4 fits the workspace.
@@ -117,9 +130,7 @@ __global__ void __launch_bounds__(WG) trtri_t_kernel(const double* __restrict__ 
       tile_at(rb, nt2 - 1 - x);
     }
   } else {
-    int cb, rb;
-    trtri_order(blockIdx.x, nt1, nt1, true, cb, rb);
-    if (cb < nt2) tile_at(rb, cb);
+    if (ocb < nt2) tile_at(orb, ocb);
   }
 }
 
@@ -130,7 +141,12 @@ __global__ void __launch_bounds__(WG) trtri_w_kernel(double* __restrict__ W, int
                                                      int h, int nblk, int groups, int64_t sw, int64_t st) {
   using Tile = MfmaTile<TS, TS, 16, false, true>;
   __shared__ __attribute__((aligned(16))) double smem[Tile::LDS_DOUBLES];
-  const int p = blockIdx.z % groups, prob = blockIdx.z / groups;
+  int p = PAIRED ? (int)(blockIdx.z % groups) : 0, orb = 0, ocb = 0;
+  const int prob = PAIRED ? (int)(blockIdx.z / groups) : (int)blockIdx.z;
+  if constexpr (!PAIRED) {
+    const int h1 = h * NB / TS;
+    trtri_order(blockIdx.x, h1, h1, groups, false, orb, ocb, p);
+  }
   W += prob * sw;
   T += prob * st;
   const int s1 = p * 2 * h, s2 = s1 + h;
@@ -179,9 +195,7 @@ __global__ void __launch_bounds__(WG) trtri_w_kernel(double* __restrict__ W, int
       tile_at(nt1 - 1 - y, cb);
     }
   } else {
-    int rb, cb;
-    trtri_order(blockIdx.x, nt1, nt1, false, rb, cb);
-    if (cb < nt2) tile_at(rb, cb);
+    if (ocb < nt2) tile_at(orb, ocb);
   }
 }
 
@@ -197,7 +211,7 @@ hipError_t launch_trtri(Context* c, int npad, const double* L, int64_t ldl, cons
     // problem size, not batch count, so a batched fit stays bit-identical to single fits.
     const int h128 = h / 2;
     if (h >= 2 && (int64_t)groups * h128 * ((h128 + 1) / 2) >= 512) {
-      const dim3 grid(h128 * h128, 1, groups * bt.count);
+      const dim3 grid(h128 * h128 * groups, 1, bt.count);
       trtri_t_kernel<128, false><<<grid, WG, 0, c->stream>>>(L, ldl, W, ldw, T, h, nblk, groups, bt.k, bt.w, bt.ws);
       trtri_w_kernel<128, false><<<grid, WG, 0, c->stream>>>(W, ldw, T, h, nblk, groups, bt.w, bt.ws);
       continue;
