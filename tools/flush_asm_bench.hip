@@ -6,6 +6,9 @@
 //   A2  the same on k-major panels (a transposed copy LT[k][i]): what the row-major staging costs
 //   A3  A1 without the seed loads (acc from zero, C - acc after the loop): what the seeding costs
 //   A4  A1 with the tile order row-major over the lower grid (no XCD chunking)
+//   A5  A1 with workgroups 256..511 (the second slot of every CU in the first round) sleeping ~half a tile first, so the
+//       two tiles of a CU never load / store at the same time (the stagger then persists)
+//   A6  A5 with a quarter-tile sleep
 // F0 / A3 must agree bit for bit, and A1 / A2 / A4 among themselves (the seeded chain rounds differently from C - acc).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form=1 -I../bayesianoptimizer_amd/csrc
 //        flush_asm_bench.hip -o flush_asm_bench
@@ -57,6 +60,11 @@ flush_v(double* __restrict__ Cm, int64_t ldc, const double* __restrict__ L, cons
     tri_decode((int)blockIdx.x, I, J);
   else
     xcd_tile((int)blockIdx.x, T, M, I, J);
+  if ((V == 5 || V == 6) && blockIdx.x >= 256 && blockIdx.x < 512) {
+    const long long t0 = wall_clock64();  // 100 MHz
+    const long long wait = V == 5 ? 5000 : 2500;  // 50 / 25 us
+    while (wall_clock64() - t0 < wait) __builtin_amdgcn_s_sleep(127);
+  }
   double* C = Cm + (int64_t)I * 128 * ldc + (int64_t)J * 128;
   using MT = MfmaTile<128, 128, 16, false, false>;
   d4 acc[4][4];
@@ -137,15 +145,17 @@ static void run(const Bufs& b, int v) {
     case 1: flush_v<1><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
     case 2: flush_v<2><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
     case 3: flush_v<3><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
-    default: flush_v<4><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
+    case 4: flush_v<4><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
+    case 5: flush_v<5><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
+    default: flush_v<6><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
   }
 }
 
 int main(int argc, char** argv) {
   const int m = argc > 1 ? atoi(argv[1]) : 15872, K = argc > 2 ? atoi(argv[2]) : 512;
   const char* names[] = {"F0 MfmaTile C-acc", "A1 asm seeded", "A2 asm seeded k-major", "A3 asm C-acc",
-                         "A4 A1 row-major order"};
-  constexpr int NV = 5;
+                         "A4 A1 row-major order", "A5 A1 + half-tile stagger", "A6 A1 + quarter stagger"};
+  constexpr int NV = 7;
   {  // bit-for-bit checks at a small size
     Bufs b = make(2048, K);
     const size_t mm = (size_t)b.m * b.m;
@@ -161,8 +171,8 @@ int main(int argc, char** argv) {
       for (size_t q = 0; q < mm; ++q) bad += out[x][q] != out[y][q];
       return bad;
     };
-    printf("m=%d K=%d: mismatches F0-A3 %zu, A1-A2 %zu, A1-A4 %zu (F0-A1 %zu: the seeded chain rounds differently)\n",
-           b.m, K, diff(0, 3), diff(1, 2), diff(1, 4), diff(0, 1));
+    printf("m=%d K=%d: mismatches F0-A3 %zu, A1-A2 %zu, A1-A4 %zu, A1-A5 %zu, A1-A6 %zu (F0-A1 %zu: the seeded chain rounds "
+           "differently)\n", b.m, K, diff(0, 3), diff(1, 2), diff(1, 4), diff(1, 5), diff(1, 6), diff(0, 1));
   }
   Bufs b = make(m, K);
   hipEvent_t e0, e1;
