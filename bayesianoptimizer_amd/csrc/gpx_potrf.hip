@@ -961,10 +961,11 @@ static void for_each_step(const Context* ctx, int nblk, int batch, int mode, int
   for (int c = 0; c < cend; ++c) {
     const bool early = c < sw;
     const bool flush = c >= 1 && c - last >= (early ? ge : (sw > 0 ? 1 : g));
-    // long flushes (K >= 256) take their tiles row-major (xmap 0): n = 16384 28.78 -> 28.60 ms (the 8 x 8 XCD chunks
-    // serve the K = 64 launches' L2 reuse; a K = 512 chunk's 16 panels are 8 MB, twice an XCD's L2;
-    // profiles/r05_flush_order_ab.log, tools/flush_asm_bench.hip A4 0.828 vs A1 0.809 of peak)
-    const int xmap = (flush && c - last >= 4) ? 0 : 1;
+    // flushes of K >= 512 take their tiles row-major (xmap 0): n = 16384 28.78 -> 28.60 ms (the 8 x 8 XCD chunks
+    // serve the shorter tiles' L2 reuse; a K = 512 chunk's 16 panels are 8 MB, twice an XCD's L2;
+    // profiles/r05_flush_order_ab.log, tools/flush_asm_bench.hip A4 0.828 vs A1 0.809 of peak).  The n = 4096 K = 256
+    // flush (one round of 465 tiles) keeps the chunks: 87.5 vs 106 us row-major (profiles/r05_potrf_launches_4096.log)
+    const int xmap = (flush && c - last >= 8) ? 0 : 1;
     f(c, step_plan(c, nblk, early ? 1 : (sw > 0 ? 0 : mode), last, flush, xmap, slots));
     if (flush) last = c;
   }
