@@ -2,6 +2,7 @@
 # Copy the outputs of tools/r05_evidence.sh (gpurun_out/ev) into profiles/ under their round-5 names.
 set -e
 cd "$(dirname "$0")/.."
+[ -s gpurun_out/ev/bench.json ] && [ -s gpurun_out/ev/bench_p4.json ] || { echo "no complete evidence set in gpurun_out/ev"; exit 1; }
 E=gpurun_out/ev
 tail -n 1 $E/bench.json > profiles/r05_bench_line.json
 tail -n 1 $E/bench_p4.json > profiles/r05_bench_line_p4.json
