@@ -208,7 +208,7 @@ hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, 
   const int nblk = npad / NB;
   const int t0 = rb0 * (rb0 + 1) / 2;  // tiles of the row blocks above rb0 are skipped (gpx_append_f64)
   const int tiles = (nblk * (nblk + 1) / 2 - t0) * bt.count;
-  // fewer tiles than CUs: split each tile's 64 rows over 4 workgroups (n = 128: 11 -> see DESIGN §5); the handle option
+  // fewer tiles than CUs: split each tile's 64 rows over 4 workgroups (n = 128: 11 -> see DESIGN_HISTORY.md); the handle option
   // GPX_OPT_GRAM_SPLIT overrides (1, 2 or 4)
   int split = tiles < 256 ? 4 : 1;
   if (c->gram_split == 1 || c->gram_split == 2 || c->gram_split == 4) split = c->gram_split;

@@ -788,7 +788,7 @@ inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush,
   }
   s.tbase = xmap ? (s.npanel + s.nlook + 7) & ~7 : s.npanel + s.nlook;  // padding workgroups exit at once
   // the overlapped pre-update shortens the panel chain but slows launches whose trailing workgroups do not all fit
-  // the co-resident slots at once
+  // the co-resident slots at once (DESIGN_HISTORY.md)
   s.overlap = slots > 0 && s.tbase + s.ntrail <= slots;
   // A long flush (K >= 256) of T tiles over S slots ends with a partial round of T mod S tiles; when that remainder fills
   // at most half the slots, its tiles run as 128 x 64 halves, so the last round takes about half a tile time
@@ -894,7 +894,7 @@ __global__ void __launch_bounds__(WG) potrf_dinv_kernel(double* __restrict__ A, 
 // B = 2: 4.86 vs 4.92 / 4.91; n = 5120 B = 4: 5.28 vs 5.41 / 5.30), at 128 blocks g = 8 beats 6 (B = 2: 9.28 vs 9.34,
 // B = 4: 16.37 vs 16.53 ms).
 // The handle options GPX_OPT_POTRF_LAZY / GPX_OPT_POTRF_MODE override.  Flushing every second launch only in the early,
-// trailing-bound launches and panel-wave priority were measured neutral (DESIGN.md §5, items 14 and the prio knob)
+// trailing-bound launches and panel-wave priority were measured neutral (DESIGN_HISTORY.md, items 14 and the prio knob)
 // and are not offered.  Trailing tiles are dealt to the XCDs in 8 x 8 super-block chunks (trail_tile xmap = 1).
 static bool batched_lookahead(int nblk, int batch) {
   return nblk <= 64 && ((batch >= 2 && nblk >= 56) || (batch >= 4 && nblk >= 48));
