@@ -609,7 +609,12 @@ def test_configs2_n16384_posterior_and_sweep_vs_oracle(engine):
     st = engine.fit(t(X), t(y), kp)
     ost = O.fit(X, y, op)
     a = st.alpha.cpu().numpy()[:n, 0]
-    assert np.abs(a - ost.alpha).max() <= 1e-8 * np.abs(ost.alpha).max()
+    # alpha = K^{-1} (y - m) is an intermediate whose rounding error scales with cond(K) (~1e7 here at noise 1e-4: the
+    # relative error of two backward-stable solves is up to ~cond(K) eps); the parity quantities built from it, mu and
+    # var, are held to 1e-9 below.  The measured alpha gap is printed so the record shows it.
+    rel = float(np.abs(a - ost.alpha).max() / np.abs(ost.alpha).max())
+    print(f"n=16384 alpha: max|d alpha| / max|alpha| = {rel:.2e}")
+    assert rel <= 1e-8, rel
     Xq = O.sobol_candidates(256, d, 5)
     mu_g, var_g = engine.posterior(st, t(Xq))
     mu_r, var_r = O.posterior(ost, Xq)
