@@ -13,6 +13,7 @@
 //                the reference's torch.cdist distances up to rounding), argmax with the lowest index among ties
 //                (torch.argmax), start index given by the caller (the reference draws it with torch.randint).
 #include <hipcub/hipcub.hpp>
+#include <climits>
 #include "gpx_internal.h"
 #include "gpx_device.h"
 
@@ -192,9 +193,107 @@ __global__ void __launch_bounds__(FPS_WG) fps_kernel(const double* __restrict__ 
   }
 }
 
+// Register-resident form (d <= DM, m <= PPT * WGS; Bayesian7's case: 8000 points, d = 5): each thread keeps its
+// points' coordinates in registers for the whole run, and each wave's winner publishes its coordinates with its (value,
+// index), so an iteration reads no global memory (fps_kernel re-reads X and the selected point every iteration:
+// ~8 us per iteration, 4.0 ms for 500 of 8000).  Same distances, same order of accumulation, same argmax and tie rule
+// (largest distance, then lowest index), so the same indices.
+template <int WGS, int PPT, int DM>
+__global__ void __launch_bounds__(WGS) fps_reg_kernel(const double* __restrict__ X, int64_t m, int d, int64_t ldx,
+                                                      int64_t k, int64_t start, int64_t* __restrict__ idx_out) {
+  constexpr int NW = WGS / 64;
+  __shared__ double sx[DM];
+  __shared__ double wv[NW], wx[NW][DM];
+  __shared__ int wi[NW];
+  __shared__ int s_sel;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  double px[PPT][DM], dist[PPT];
+#pragma unroll
+  for (int q = 0; q < PPT; ++q) {
+    const int64_t p = (int64_t)q * WGS + t;
+#pragma unroll
+    for (int j = 0; j < DM; ++j) px[q][j] = (p < m && j < d) ? X[p * ldx + j] : 0.0;
+    dist[q] = -INFINITY;  // points beyond m never win
+  }
+  if (t < DM) sx[t] = t < d ? X[start * ldx + t] : 0.0;
+  __syncthreads();
+  int sel = (int)start;
+  for (int64_t it = 0; it < k; ++it) {
+    if (t == 0) idx_out[it] = sel;
+    double s[DM];
+#pragma unroll
+    for (int j = 0; j < DM; ++j) s[j] = sx[j];
+    double bv = -INFINITY;
+    int bi = INT_MAX;
+#pragma unroll
+    for (int q = 0; q < PPT; ++q) {
+      const int p = q * WGS + t;
+      if (p < m) {
+        double d2 = 0.0;
+#pragma unroll
+        for (int j = 0; j < DM; ++j) {
+          if (j < d) {
+            const double df = px[q][j] - s[j];
+            d2 += df * df;
+          }
+        }
+        dist[q] = (it == 0) ? d2 : fmin(dist[q], d2);
+        if (dist[q] > bv) {  // q ascending -> p ascending within a thread: strict '>' keeps the lowest index
+          bv = dist[q];
+          bi = p;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double v2 = __shfl_xor(bv, o);
+      const int i2 = __shfl_xor(bi, o);
+      if (v2 > bv || (v2 == bv && i2 < bi)) {
+        bv = v2;
+        bi = i2;
+      }
+    }
+    if (lane == 0) {
+      wv[w] = bv;
+      wi[w] = bi;
+    }
+    if (bi != INT_MAX && t == bi % WGS) {  // the wave's winner publishes its coordinates
+      const int qw = bi / WGS;
+#pragma unroll
+      for (int q = 0; q < PPT; ++q)
+        if (q == qw)
+#pragma unroll
+          for (int j = 0; j < DM; ++j) wx[w][j] = px[q][j];
+    }
+    __syncthreads();
+    if (w == 0) {  // the NW wave winners: largest value, then lowest index
+      double v = lane < NW ? wv[lane] : -INFINITY;
+      int i = lane < NW ? wi[lane] : INT_MAX, src = lane < NW ? lane : 0;
+#pragma unroll
+      for (int o = NW / 2; o > 0; o >>= 1) {
+        const double v2 = __shfl_xor(v, o);
+        const int i2 = __shfl_xor(i, o), s2 = __shfl_xor(src, o);
+        if (v2 > v || (v2 == v && i2 < i)) {
+          v = v2;
+          i = i2;
+          src = s2;
+        }
+      }
+      if (lane < DM) sx[lane] = wx[src][lane];
+      if (lane == 0) s_sel = i;
+    }
+    __syncthreads();
+    sel = s_sel;
+  }
+}
+
 hipError_t launch_fps(Context* c, const double* X, int64_t m, int d, int64_t ldx, int64_t k, int64_t start,
                       int64_t* idx_out) {
-  if (m <= 8 * FPS_WG)
+  if (m <= 8 * FPS_WG && d <= 4)
+    fps_reg_kernel<FPS_WG, 8, 4><<<1, FPS_WG, 0, c->stream>>>(X, m, d, ldx, k, start, idx_out);
+  else if (m <= 8 * FPS_WG && d <= 5)  // 512 threads: 16 points of up to 5 coordinates per thread fit the registers
+    fps_reg_kernel<512, 16, 5><<<1, 512, 0, c->stream>>>(X, m, d, ldx, k, start, idx_out);
+  else if (m <= 8 * FPS_WG)
     fps_kernel<8><<<1, FPS_WG, 0, c->stream>>>(X, m, d, ldx, k, start, idx_out);
   else if (m <= 32 * FPS_WG)
     fps_kernel<32><<<1, FPS_WG, 0, c->stream>>>(X, m, d, ldx, k, start, idx_out);

@@ -278,10 +278,20 @@ static_assert(TrmmTile::LDS_DOUBLES * 8 == trmm_asm::LDS_BYTES, "hand-placed til
 
 // kfull = 0: W upper triangular (k < (I+1)*128); kfull = 1: W is a full npad x npad matrix (the SVGP's
 // W2 = L^{-T} S term, gpx_svgp.hip), k over all nI row tiles.
+// With W2 (the SVGP's second product, grid.y = 2): blockIdx.y = 0 runs W2 with kfull = 1 into ss2 (the heavier,
+// full-k tiles dispatched first), blockIdx.y = 1 the product given by (W, ss_part, kfull): both products of a chunk in
+// one launch share its K* and one launch tail (two launches before).
 __global__ void __launch_bounds__(WG) trmm_sumsq_kernel(const double* __restrict__ W, int64_t ldw,
                                                         const double* __restrict__ kstar, int64_t C, int nI, int ncb,
-                                                        double* __restrict__ ss_part, int kfull) {
+                                                        double* __restrict__ ss_part, int kfull,
+                                                        const double* __restrict__ W2 = nullptr,
+                                                        double* __restrict__ ss2 = nullptr) {
   __shared__ __attribute__((aligned(16))) double smem[TrmmTile::LDS_DOUBLES];
+  if (W2 && blockIdx.y == 0) {
+    W = W2;
+    ss_part = ss2;
+    kfull = 1;
+  }
   // Candidate tiles in groups of G = 64 (every row tile of a group, heaviest first, before the next group), and inside a
   // group XCD-aware: workgroups b, b+8, ... share an XCD (dispatch is round-robin; speed only, never correctness), so
   // XCD x gets the group's candidate tiles cb = x (mod 8) and walks them row tile by row tile.  Groups keep the K*
@@ -790,8 +800,7 @@ hipError_t launch_svgp_chunk(Context* c, const gpx_kernel_params& p, double min_
   {
     LaunchTimer tm(c, GPX_TIMER_TRMM);
     const int ncbt = (int)((m_chunk + TT - 1) / TT);
-    trmm_sumsq_kernel<<<ncbt * nI, WG, 0, c->stream>>>(W, ldw, b.kstar, C, nI, ncbt, b.ss_part, 0);
-    trmm_sumsq_kernel<<<ncbt * nI, WG, 0, c->stream>>>(W2, ldw, b.kstar, C, nI, ncbt, ss2, 1);
+    trmm_sumsq_kernel<<<dim3(ncbt * nI, 2), WG, 0, c->stream>>>(W, ldw, b.kstar, C, nI, ncbt, b.ss_part, 0, W2, ss2);
   }
   {
     LaunchTimer tm(c, GPX_TIMER_ACQ);
