@@ -14,6 +14,7 @@
 // with the O(n) terms (quadratic form, log-determinant, mean gradient).
 #include "gpx_internal.h"
 #include "gpx_device.h"
+#include "gpx_trmm_asm.h"
 #include <algorithm>
 #include <cstdlib>
 
@@ -45,6 +46,7 @@ __global__ void __launch_bounds__(WG) mll_grad_kernel(gpx_kernel_params p, int n
   constexpr int SW = 16, KVP = SW + 1, XP = DMAX + 1;
   constexpr int EPI = 2 * MT * XP + 2 * MT * GPX_MAX_RHS + MT * KVP;
   constexpr int SMEM = EPI > Tile::LDS_DOUBLES ? EPI : Tile::LDS_DOUBLES;  // 73.7 KB for d <= 16
+  static_assert(Tile::LDS_DOUBLES * 8 == trmm_asm::LDS_BYTES, "hand-placed tile uses MfmaTile's LDS image");
   __shared__ __attribute__((aligned(16))) double smem[SMEM];
   int I, J;
   tri_decode(blockIdx.x, I, J);
@@ -63,8 +65,11 @@ __global__ void __launch_bounds__(WG) mll_grad_kernel(gpx_kernel_params p, int n
   }
   const int kend = min(kbeg + kc, npad);
   const double aa = (blockIdx.y == 0) ? 1.0 : 0.0;
-  Tile t;
-  t.run(W + (int64_t)i0 * ldw, ldw, W + (int64_t)j0 * ldw, ldw, kbeg, kend, smem);  // ends with a barrier
+  // the hand-placed k loop of gpx_trmm_asm.h (row-major operands, the Cholesky's flush tile): same MFMA sequence per
+  // accumulator as MfmaTile::run, so the same bits; ends with a barrier
+  trmm_asm::TileT<false, false> t;
+  t.zero();
+  t.run(W + (int64_t)i0 * ldw + kbeg, ldw, W + (int64_t)j0 * ldw + kbeg, ldw, (kend - kbeg) / 16, smem);
 
   // ---- epilogue: stage raw X rows and alpha of both tile sides in LDS
   double* xi = smem;             // [MT][XP]
