@@ -16,6 +16,7 @@
 #include <climits>
 #include "gpx_internal.h"
 #include "gpx_device.h"
+#include "gpx_trmm_asm.h"
 
 namespace gpx {
 
@@ -45,7 +46,8 @@ hipError_t launch_svgp_pad(Context* c, int ntask, int M, int Mpad, const double*
 }
 
 // W2[k][i] = sum_{j >= max(k0, i0)} W[k][j] S[j][i] for the 128x128 tile (k0, i0); W upper, S lower.
-using W2Tile = MfmaTile<128, 128, 16, false, true>;
+using W2Tile = MfmaTile<128, 128, 16, false, true>;  // (its accumulator layout and LDS size)
+static_assert(W2Tile::LDS_DOUBLES * 8 == trmm_asm::LDS_BYTES, "hand-placed tile uses MfmaTile's LDS image");
 
 __global__ void __launch_bounds__(WG) svgp_w2_kernel(int Mpad, const double* __restrict__ W,
                                                      const double* __restrict__ S, int64_t s_stride,
@@ -58,9 +60,11 @@ __global__ void __launch_bounds__(WG) svgp_w2_kernel(int Mpad, const double* __r
   const int R = blockIdx.x / nt, Cc = blockIdx.x % nt;
   const int k0 = R * 128, i0 = Cc * 128;
   const int kbeg = k0 > i0 ? k0 : i0;
-  W2Tile tile;
-  // A(m, j) = W[k0 + m][j] (row-major), B(j, n) = S[j][i0 + n] (k-major)
-  tile.run(W + off + (int64_t)k0 * Mpad, Mpad, S + i0, Mpad, kbeg, Mpad, smem);
+  // A(m, j) = W[k0 + m][j] (row-major), B(j, n) = S[j][i0 + n] (k-major), on the hand-placed k loop (gpx_trmm_asm.h:
+  // the same MFMA sequence per accumulator as MfmaTile::run, so the same bits)
+  trmm_asm::TileT<false, true> tile;
+  tile.zero();
+  tile.run(W + off + (int64_t)k0 * Mpad + kbeg, Mpad, S + i0 + (int64_t)kbeg * Mpad, Mpad, (Mpad - kbeg) / 16, smem);
   double* O = W2 + off + (int64_t)k0 * Mpad + i0;
 #pragma unroll
   for (int i = 0; i < W2Tile::WM; ++i)
