@@ -123,7 +123,11 @@ def test_topk_matches_oracle_with_ties_and_nan(engine):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("m,d,k,start", [(8000, 5, 500, 1234), (3000, 2, 300, 0), (20000, 8, 64, 19999),
-                                         (9, 1, 5, 0)])
+                                         (9, 1, 5, 0),
+                                         # the register-resident kernels' edges (gpx_svgp.hip launch_fps): 1024 x 8
+                                         # points at d <= 4, 512 x 16 at d = 5, the re-reading kernel beyond
+                                         (8192, 4, 200, 8191), (8192, 5, 200, 0), (8193, 5, 50, 8192),
+                                         (1024, 6, 100, 7), (64, 3, 64, 5)])
 def test_fps_matches_oracle(engine, m, d, k, start):
     X = np.random.default_rng(m + d).random((m, d))
     if m == 9:
