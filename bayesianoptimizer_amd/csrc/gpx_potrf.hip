@@ -961,11 +961,12 @@ static void for_each_step(const Context* ctx, int nblk, int batch, int mode, int
   for (int c = 0; c < cend; ++c) {
     const bool early = c < sw;
     const bool flush = c >= 1 && c - last >= (early ? ge : (sw > 0 ? 1 : g));
-    // flushes of K >= 512 take their tiles row-major (xmap 0): n = 16384 28.78 -> 28.60 ms (the 8 x 8 XCD chunks
-    // serve the shorter tiles' L2 reuse; a K = 512 chunk's 16 panels are 8 MB, twice an XCD's L2;
-    // profiles/r05_flush_order_ab.log, tools/flush_asm_bench.hip A4 0.828 vs A1 0.809 of peak).  The n = 4096 K = 256
+    // flushes of K >= 384 take their tiles row-major (xmap 0): n = 16384 (K = 512) 28.78 -> 28.60 ms (the 8 x 8 XCD
+    // chunks serve the shorter tiles' L2 reuse; a K = 512 chunk's 16 panels are 8 MB, twice an XCD's L2;
+    // profiles/r05_flush_order_ab.log, tools/flush_asm_bench.hip A4 0.828 vs A1 0.809 of peak); K = 384: n = 8192
+    // 5.673 -> 5.629 ms, B = 4 x n = 4096 3.169 -> 3.163 (profiles/r05_flush_order_384_ab.log).  The n = 4096 K = 256
     // flush (one round of 465 tiles) keeps the chunks: 87.5 vs 106 us row-major (profiles/r05_potrf_launches_4096.log)
-    const int xmap = (flush && c - last >= 8) ? 0 : 1;
+    const int xmap = (flush && c - last >= 6) ? 0 : 1;
     f(c, step_plan(c, nblk, early ? 1 : (sw > 0 ? 0 : mode), last, flush, xmap, slots));
     if (flush) last = c;
   }
