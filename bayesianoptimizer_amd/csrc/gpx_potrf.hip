@@ -941,9 +941,11 @@ static int potrf_switch(const Context* ctx, int nblk, int batch, int mode, int g
   if (ctx->potrf_mode >= 0 || ctx->potrf_lazy > 0) return 0;
   if (batch != 1) {
     // batches on the lookahead schedule finish on the eager one for their last ~16 block columns (B = 4, n = 4096:
-    // 3.195 -> 3.149 ms with the switch at 49, 3.153 at 37, 3.219 at 25; profiles/r05_potrf_schedules.log)
+    // 3.195 -> 3.149 ms with the switch at 49, 3.153 at 37, 3.219 at 25; profiles/r05_potrf_schedules.log): the
+    // launch after the last flush at or before nblk - 16 for B >= 4 (g = 6: 49 vs 43 3.118 vs 3.135 ms in a sweep, 3.155 vs 3.165 B = 4 and 5.353 vs 5.362 B = 8 in an A/B,
+    // profiles/r05_potrf_batched_switch_ab.log), one launch earlier for B = 2 (g = 4: 45; 49 measured 2.138 vs 2.133)
     if (!batched_lookahead(nblk, batch)) return 0;
-    return ((nblk - 16 - 1) / g) * g + 1;
+    return ((nblk - (batch >= 4 ? 16 : 17)) / g) * g + 1;
   }
   if (mode == 0) return nblk == 64 ? 9 : 0;
   if (nblk - kEagerTail < g + 1) return 0;
