@@ -11,7 +11,9 @@ Prints ONE JSON line on rank 0.  value = candidates scored per second over the w
 loop and reported beside it.  Inputs are resident in HBM before the timed region starts.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
+       N>1 either under a launcher (python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ...
+       bench.py --gpus N: WORLD_SIZE must equal N) or bare: `python bench.py --gpus N` then starts the N ranks itself
+       (launch_ranks) before anything in this process touches the GPU, so n_gpus = N by construction.
 """
 from __future__ import annotations
 
@@ -35,7 +37,7 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix, spec; measured 78.1 TF/s (profil
 HBM_PEAK_GBS = 8000.0
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -52,7 +54,34 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-other-configs", action="store_true",
                     help="skip the side measurements of BASELINE configs[2] and configs[4] (N=1 only)")
-    return ap.parse_args()
+    ap.add_argument("--launcher-selftest", action="store_true",
+                    help="test hook: every rank reports its rank variables and exits before any GPU call")
+    return ap.parse_args(argv)
+
+
+def launch_ranks(gpus: int, argv) -> int:
+    """`bench.py --gpus N` without a launcher around it: run N ranks of this script under torch.distributed.run
+    (one process per GPU, rendezvous on 127.0.0.1, a free port) as a CHILD process and return its exit status.  Called
+    before this process makes any HIP call (no GPEngine, no torch.cuda query): the children own the GPUs."""
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")  # torch.distributed.run's default for N > 1, stated to keep it quiet
+    return subprocess.call(cmd, env=env)
+
+
+def check_world(args) -> None:
+    """Under a launcher the world it started must be the one --gpus names (the driver passes both)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; launch N ranks for --gpus N "
+                         f"(or run bare: bench.py --gpus N starts them itself)")
 
 
 def dist_setup(args):
@@ -90,8 +119,10 @@ def pmc_traffic_record():
             rec = json.load(f)
     except Exception:
         return None, None
-    src = {"file": PMC_TRAFFIC_FILE, "generated_utc": rec.get("generated_utc"), "dispatches": rec.get("dispatches"),
-           "passes": rec.get("passes")}
+    # "recorded": read from the PMC passes' file, not measured by this process (rocprofv3 --pmc cannot run inside it);
+    # the evidence script regenerates the file in the same call, on the same box and tree, right before its bench line
+    src = {"kind": "recorded", "file": PMC_TRAFFIC_FILE, "generated_utc": rec.get("generated_utc"),
+           "dispatches": rec.get("dispatches"), "passes": rec.get("passes")}
     return rec.get("hbm_bytes_per_launch"), src
 
 
@@ -416,8 +447,21 @@ def other_configs(eng, dev, seed):
     return out
 
 
-def main():
-    args = parse()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        rc = launch_ranks(args.gpus, argv)
+        if args.launcher_selftest:
+            print(json.dumps({"launcher": {"gpus": args.gpus, "rc": rc,
+                                           "parent_hip_initialized": bool(torch.cuda.is_initialized())}}))
+        sys.exit(rc)
+    check_world(args)
+    if args.launcher_selftest:
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                          "world_size": int(os.environ.get("WORLD_SIZE", "1")),
+                          "hip_initialized": bool(torch.cuda.is_initialized())}), flush=True)
+        return
     dist, rank, world, local = dist_setup(args)
     dev = torch.device("cuda", local)
     P = args.problems_per_gpu
