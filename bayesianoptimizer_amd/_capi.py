@@ -139,6 +139,12 @@ _PROTOS = {
     "gpx_fit_batched_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, c_int64, _p, c_int64, c_int64, _p,
                                       c_int64, c_int64, c_int64, _p, c_int64, c_int64, _p, c_int64, _p, c_int64,
                                       c_int64, _p, c_int64, _p, _p, c_size_t]),
+    "gpx_fit_batched_params_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, c_int64, _p, c_int64, c_int64, _p,
+                                             c_int64, c_int64, c_int64, _p, c_int64, c_int64, _p, c_int64, _p, c_int64,
+                                             c_int64, _p, c_int64, _p, _p, c_size_t]),
+    "gpx_fit_factor_batched_params_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, c_int64, _p, c_int64, c_int64,
+                                                    _p, c_int64, c_int64, c_int64, _p, c_int64, c_int64, _p, c_int64,
+                                                    _p, c_int64, _p, _p, c_size_t]),
     "gpx_potrs_workspace_size": (c_int32, [c_int64, c_int64, POINTER(c_size_t)]),
     "gpx_potrs_f64": (c_int32, [_h, c_int64, _p, c_int64, _p, _p, c_int64, c_int64, c_double, _p, _p, _p, c_size_t]),
     "gpx_fit_factor_workspace_size": (c_int32, [c_int64, c_int64, POINTER(c_size_t)]),
@@ -161,6 +167,11 @@ _PROTOS = {
     "gpx_acquire_argmax_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, _p, _p,
                                          c_int64, c_int64, POINTER(AcqParamsC), c_int64, _p, _p, _p, _p,
                                          c_size_t]),
+    "gpx_sweep_multi_workspace_size": (c_int32, [c_int64, c_int64, POINTER(c_size_t)]),
+    "gpx_acquire_argmax_multi_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, c_int64, _p, c_int64,
+                                               POINTER(c_void_p), POINTER(c_int64), POINTER(c_void_p),
+                                               POINTER(c_double), POINTER(c_double), POINTER(c_double), _p, c_int64,
+                                               c_int64, POINTER(AcqParamsC), c_int64, _p, _p, _p, _p, c_size_t]),
     "gpx_argmax_combine_f64": (c_int32, [_h, _p, _p, c_int64, _p, _p]),
     "gpx_comm_unique_id": (c_int32, [c_void_p]),
     "gpx_comm_init": (c_int32, [_h, c_void_p, c_int32, c_int32, POINTER(c_void_p)]),
@@ -170,6 +181,9 @@ _PROTOS = {
     "gpx_mll_workspace_size": (c_int32, [c_int64, POINTER(c_size_t)]),
     "gpx_mll_grad_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, _p, c_int64, _p, c_int64, c_int64, _p,
                                    c_int64, _p, c_int64, _p, _p, _p, c_size_t]),
+    "gpx_mll_grad_batched_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, c_int64, _p, c_int64, c_int64, _p,
+                                           c_int64, c_int64, c_int64, _p, c_int64, c_int64, _p, c_int64, c_int64, _p,
+                                           c_int64, _p, _p, c_size_t]),
     "gpx_svgp_prepare_workspace_size": (c_int32, [c_int64, c_int64, POINTER(c_size_t)]),
     "gpx_svgp_prepare_f64": (c_int32, [_h, POINTER(KernelParamsC), c_int64, c_int64, c_double, _p, c_int64, c_int64,
                                        _p, c_int64, _p, c_int64, c_int64, _p, _p, _p, _p, _p, c_size_t]),

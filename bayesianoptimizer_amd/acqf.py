@@ -69,12 +69,14 @@ class _Moments(torch.autograd.Function):
 
 class _Objective:
     """Scalar objective of the model's outputs in original units: a linear combination (LinearMCObjective,
-    Bayesian2.py:213-214) or one output.  The outputs share the covariance, so the objective is Gaussian with mean
-    sum_t w_t (y_mean_t + s_t mu_t) and covariance (sum_t w_t^2 s_t^2) Sigma_std."""
+    Bayesian2.py:213-214) or one output, as a sum of Gaussian terms (state, alpha, mean scale, variance scale) plus an
+    offset.  Shared covariance (one factorisation): ONE term, the objective's mean sum_t w_t (y_mean_t + s_t mu_t) from
+    the combined alpha and its covariance (sum_t w_t^2 s_t^2) Sigma_std.  Independent outputs (ExactGP independent
+    mode, the multi-output SingleTaskGP): one term per output with a non-zero weight — mean sum_t w_t s_t mu_t + sum_t
+    w_t y_mean_t, covariance sum_t w_t^2 s_t^2 Sigma_t (the outputs are independent a posteriori)."""
 
     def __init__(self, model, weights: Optional[Sequence[float]] = None, output: int = 0):
-        st = model.state
-        T = st.nrhs
+        T = model.num_outputs
         w = torch.zeros(T, dtype=torch.float64)
         if weights is not None:
             w = torch.as_tensor(weights, dtype=torch.float64).reshape(-1)
@@ -85,21 +87,41 @@ class _Objective:
         ym, ys = model._untransform()
         ym = torch.tensor(ym if ym is not None else [0.0] * T, dtype=torch.float64)
         ys = torch.tensor(ys if ys is not None else [1.0] * T, dtype=torch.float64)
+        ws = w * ys
+        self.terms = []
+        if getattr(model, "independent", False):
+            for t in range(T):
+                if float(ws[t]) != 0.0:
+                    st = model.states[t]
+                    self.terms.append((st, st.alpha[:, 0].contiguous(), float(ws[t]), float(ws[t]) ** 2))
+            self.offset = float((w * ym).sum())
+            self.var_scale = float((ws * ws).sum())
+            return
+        st = model.state
         dev = st.alpha.device
-        ws = (w * ys).to(dev)
-        self.alpha = (st.alpha * ws.unsqueeze(0)).sum(dim=1).contiguous()
+        alpha = (st.alpha * ws.to(dev).unsqueeze(0)).sum(dim=1).contiguous()
         cm = float(st.params.const_mean)
-        self.offset = float((w * ym).sum()) + cm * (float((w * ys).sum()) - 1.0)
-        self.var_scale = float((w * w * ys * ys).sum())
+        self.offset = float((w * ym).sum()) + cm * (float(ws.sum()) - 1.0)
+        self.var_scale = float((ws * ws).sum())
+        self.terms.append((st, alpha, 1.0, self.var_scale))
 
 
-def posterior_moments(model, X: torch.Tensor, objective: Optional[_Objective] = None):
+def posterior_moments(model, X: torch.Tensor, objective: Optional[_Objective] = None, floor_terms: bool = False):
     """Mean (B, q) and covariance (B, q, q) of the objective at X (B, q, d), differentiable w.r.t. X (noise-free
-    posterior, like BoTorch's acquisition functions).  ``model``: a fitted models.ExactGP."""
+    posterior, like BoTorch's acquisition functions).  ``model``: a fitted models.ExactGP.  ``floor_terms`` (q = 1):
+    each term's standardised variance floored at GPyTorch's 1e-10 before scaling, as the GPU sweep does."""
     obj = objective or _Objective(model)
     B, q, d = X.shape
-    mean, cov = _Moments.apply(X.reshape(B * q, d), model.engine, model.state, q, obj.alpha)
-    return mean.reshape(B, q) + obj.offset, cov.reshape(B, q, q) * obj.var_scale
+    mean_t = torch.full((B, q), obj.offset, dtype=torch.float64, device=X.device)
+    cov_t = torch.zeros((B, q, q), dtype=torch.float64, device=X.device)
+    for st, alpha, ms, vs in obj.terms:
+        mean, cov = _Moments.apply(X.reshape(B * q, d), model.engine, st, q, alpha)
+        cov = cov.reshape(B, q, q)
+        if floor_terms:
+            cov = torch.clamp(cov, min=GPYTORCH_MIN_VAR_F64)
+        mean_t = mean_t + ms * mean.reshape(B, q)
+        cov_t = cov_t + vs * cov
+    return mean_t, cov_t
 
 
 # ---- smooth maths (BoTorch safe_math [upstream], restated) -----------------------------------------------------
@@ -208,10 +230,9 @@ class AnalyticAcquisition:
             X = X.unsqueeze(1)
         if X.shape[1] != 1:
             raise ValueError("analytic acquisition functions take q = 1 (X: B x 1 x d)")
-        mu, cov = posterior_moments(self.model, X, self.objective)
+        mu, cov = posterior_moments(self.model, X, self.objective, floor_terms=True)
         mu = mu[:, 0]
-        var_std = torch.clamp(cov[:, 0, 0] / self.objective.var_scale, min=GPYTORCH_MIN_VAR_F64)
-        var = torch.clamp(var_std * self.objective.var_scale, min=BOTORCH_MIN_VAR)
+        var = torch.clamp(cov[:, 0, 0], min=BOTORCH_MIN_VAR)
         sigma = torch.sqrt(var)
         if self.kind == "variance":
             return var

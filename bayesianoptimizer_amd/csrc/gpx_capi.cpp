@@ -573,24 +573,47 @@ static size_t fit_slice_bytes(int64_t npad, int64_t nrhs) {
   return ((a > b ? a : b) + 255) & ~(size_t)255;
 }
 
+// Bytes at the end of a batched fit's workspace for the per-problem constant means (Batch::means) of a fit whose
+// problems carry their own kernel parameters.
+static size_t means_bytes(int64_t batch) { return ((size_t)batch * 8 + 255) & ~(size_t)255; }
+
 gpx_status gpx_fit_batched_workspace_size(int64_t n, int64_t nrhs, int64_t batch, size_t* bytes) {
   if (!bytes || n < 1 || nrhs < 1 || nrhs > GPX_MAX_RHS || batch < 1 || batch > 65535) return GPX_INVALID_ARG;
-  *bytes = fit_slice_bytes(padded(n), nrhs) * (size_t)batch + 256;
+  *bytes = fit_slice_bytes(padded(n), nrhs) * (size_t)batch + means_bytes(batch) + 256;
   return GPX_OK;
 }
 
-// Batched posterior updates; W == nullptr: factor + triangular solves only (gpx_fit_factor_batched_f64).
-static gpx_status fit_batched_impl(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n, const double* X,
-                                   int64_t ldx, int64_t stride_x, const double* Y, int64_t ldy, int64_t stride_y,
-                                   int64_t nrhs, double* K, int64_t ldk, int64_t stride_k, double* Dinv,
-                                   int64_t stride_dinv, double* W, int64_t ldw, int64_t stride_w, double* alpha,
-                                   int64_t stride_alpha, int32_t* info, void* ws, size_t ws_bytes) {
+gpx_status gpx_fit_factor_batched_workspace_size(int64_t n, int64_t nrhs, int64_t batch, size_t* bytes) {
+  if (!bytes || n < 1 || nrhs < 1 || nrhs > GPX_MAX_RHS || batch < 1 || batch > 65535) return GPX_INVALID_ARG;
+  *bytes = ((gpx::potrs_workspace_bytes(padded(n), nrhs, batch) + 255) & ~(size_t)255) + means_bytes(batch) + 256;
+  return GPX_OK;
+}
+
+// Batched posterior updates; W == nullptr: factor + triangular solves only (gpx_fit_factor_batched_f64).  p points to
+// one gpx_kernel_params (pstep = 0: shared by every problem) or to `batch` of them (pstep = 1, the
+// gpx_fit_*_batched_params_f64 entry points).  Per-problem parameters that differ are served by one Gram launch per
+// problem (its covariance parameters as kernel arguments; each launch fills the GPU from n ~ 1000 on) which also writes
+// the problem's constant mean into the workspace for the solves; the Cholesky, the forward / backward solves and the
+// inverse stay ONE set of launches over all problems (the latency-bound chain is what batching amortises).
+static gpx_status fit_batched_impl(gpx_handle h, const gpx_kernel_params* p, int64_t pstep, int64_t batch, int64_t n,
+                                   const double* X, int64_t ldx, int64_t stride_x, const double* Y, int64_t ldy,
+                                   int64_t stride_y, int64_t nrhs, double* K, int64_t ldk, int64_t stride_k,
+                                   double* Dinv, int64_t stride_dinv, double* W, int64_t ldw, int64_t stride_w,
+                                   double* alpha, int64_t stride_alpha, int32_t* info, void* ws, size_t ws_bytes) {
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return GPX_INVALID_ARG;
   const bool inverse = W != nullptr;
-  GPX_TRY(check_params(c, p));
-  GPX_TRY(check_n(c, n));
   if (batch < 1 || batch > 65535) return fail(c, GPX_INVALID_ARG, "batch must be in [1, 65535]");
+  GPX_NONNULL(c, p);
+  bool shared = true;
+  for (int64_t b = 0; b < (pstep ? batch : 1); ++b) {
+    const gpx_status st = check_params(c, p + b);
+    if (st != GPX_OK) return fail(c, st, "problem " + std::to_string(b) + ": " + c->last_error);
+    if (p[b].d != p[0].d)
+      return fail(c, GPX_INVALID_ARG, "every problem of a batched fit needs the same input dimension d");
+    if (b > 0 && std::memcmp(p + b, p, sizeof(gpx_kernel_params)) != 0) shared = false;
+  }
+  GPX_TRY(check_n(c, n));
   if (nrhs < 1 || nrhs > GPX_MAX_RHS) return fail(c, GPX_INVALID_ARG, "nrhs must be in [1, 8]");
   GPX_NONNULL(c, X);
   GPX_NONNULL(c, Y);
@@ -606,9 +629,12 @@ static gpx_status fit_batched_impl(gpx_handle h, const gpx_kernel_params* p, int
   if (inverse) GPX_TRY(check_ld(c, ldw, npad, "W", true));
   const int64_t nblk = npad / gpx::NB;
   if (batch > 1) {
-    // problems must not overlap (a stride of 0 would make them race on the same output)
-    if (stride_x < n * ldx || stride_y < n * ldy || stride_k < npad * ldk || (inverse && stride_w < npad * ldw) ||
-        stride_dinv < 2 * nblk * gpx::NB * gpx::NB || stride_alpha < npad * nrhs)
+    // outputs must not overlap (a stride of 0 would make the problems race on the same output); the read-only inputs
+    // may be shared (stride 0: one X for the T outputs of a multi-output model) or interleaved (Y stride 1, ldy = T:
+    // output column b of an n x T target matrix)
+    if (stride_x < 0 || stride_y < 0) return fail(c, GPX_INVALID_ARG, "X / Y strides must be >= 0");
+    if (stride_k < npad * ldk || (inverse && stride_w < npad * ldw) || stride_dinv < 2 * nblk * gpx::NB * gpx::NB ||
+        stride_alpha < npad * nrhs)
       return fail(c, GPX_INVALID_ARG, "batch strides smaller than one problem");
     if ((stride_k | (inverse ? stride_w : 0) | stride_dinv) & 1)
       return fail(c, GPX_INVALID_ARG, "K/W/Dinv strides must be even");
@@ -630,12 +656,25 @@ static gpx_status fit_batched_impl(gpx_handle h, const gpx_kernel_params* p, int
   bt.alpha = stride_alpha;
   bt.ws = (int64_t)(fit_slice_bytes(npad, nrhs) / sizeof(double));
   double* slice = align256(ws);
-  // the gram kernel clears info[0 .. batch) before the Cholesky (no separate memset dispatch)
-  // the Gram launch also clears the triangular solve's hand-off granules of a factor-only fit (no memset dispatch)
-  GPX_TRY(hip_check(c, gpx::launch_gram(c, *p, (int)n, (int)npad, X, ldx, K, ldk, bt, 0, info,
-                                        inverse ? nullptr : slice,
-                                        inverse ? 0 : gpx::potrs_clear_bytes(npad, nrhs, batch)),
-                    "gram"));
+  // per-problem constant means after the solves' part of the workspace
+  const size_t solve_bytes = inverse ? fit_slice_bytes(npad, nrhs) * (size_t)batch
+                                     : ((gpx::potrs_workspace_bytes(npad, nrhs, batch) + 255) & ~(size_t)255);
+  double* means = shared ? nullptr : reinterpret_cast<double*>(reinterpret_cast<char*>(slice) + solve_bytes);
+  bt.means = means;
+  // the gram kernel clears info[0 .. batch) before the Cholesky (no separate memset dispatch), and in a factor-only fit
+  // the triangular solve's hand-off granules of every problem
+  void* zero = inverse ? nullptr : slice;
+  const size_t zero_bytes = inverse ? 0 : gpx::potrs_clear_bytes(npad, nrhs, batch);
+  if (shared) {
+    GPX_TRY(hip_check(c, gpx::launch_gram(c, *p, (int)n, (int)npad, X, ldx, K, ldk, bt, 0, info, zero, zero_bytes),
+                      "gram"));
+  } else {
+    for (int64_t b = 0; b < batch; ++b)
+      GPX_TRY(hip_check(c, gpx::launch_gram(c, p[b], (int)n, (int)npad, X + b * stride_x, ldx, K + b * stride_k, ldk,
+                                            gpx::Batch(), 0, info + b, b == 0 ? zero : nullptr, b == 0 ? zero_bytes : 0,
+                                            means + b),
+                        "gram"));
+  }
   if (!inverse) {
     // factor + forward substitution (dataflow schedule), then the backward half of the solve
     gpx::ForwardRhs fr;
@@ -645,6 +684,7 @@ static gpx_status fit_batched_impl(gpx_handle h, const gpx_kernel_params* p, int
     fr.nrhs = (int)nrhs;
     fr.n = (int)n;
     fr.mean = p->const_mean;
+    fr.means = means;
     fr.buf = reinterpret_cast<double*>(reinterpret_cast<char*>(slice) + gpx::potrs_forward_offset(npad, nrhs, batch));
     bool z_done = false;
     GPX_TRY(hip_check(c, gpx::launch_potrf(c, (int)npad, K, ldk, Dinv, info, bt, nullptr, 0, &fr, &z_done), "potrf"));
@@ -670,14 +710,8 @@ gpx_status gpx_fit_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t
   Context* c = reinterpret_cast<Context*>(h);
   if (!c) return GPX_INVALID_ARG;
   GPX_NONNULL(c, W);
-  return fit_batched_impl(h, p, batch, n, X, ldx, stride_x, Y, ldy, stride_y, nrhs, K, ldk, stride_k, Dinv,
+  return fit_batched_impl(h, p, 0, batch, n, X, ldx, stride_x, Y, ldy, stride_y, nrhs, K, ldk, stride_k, Dinv,
                           stride_dinv, W, ldw, stride_w, alpha, stride_alpha, info, ws, ws_bytes);
-}
-
-gpx_status gpx_fit_factor_batched_workspace_size(int64_t n, int64_t nrhs, int64_t batch, size_t* bytes) {
-  if (!bytes || n < 1 || nrhs < 1 || nrhs > GPX_MAX_RHS || batch < 1 || batch > 65535) return GPX_INVALID_ARG;
-  *bytes = gpx::potrs_workspace_bytes(padded(n), nrhs, batch) + 256;
-  return GPX_OK;
 }
 
 gpx_status gpx_fit_factor_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n,
@@ -685,7 +719,28 @@ gpx_status gpx_fit_factor_batched_f64(gpx_handle h, const gpx_kernel_params* p, 
                                       int64_t stride_y, int64_t nrhs, double* K, int64_t ldk, int64_t stride_k,
                                       double* Dinv, int64_t stride_dinv, double* alpha, int64_t stride_alpha,
                                       int32_t* info, void* ws, size_t ws_bytes) {
-  return fit_batched_impl(h, p, batch, n, X, ldx, stride_x, Y, ldy, stride_y, nrhs, K, ldk, stride_k, Dinv,
+  return fit_batched_impl(h, p, 0, batch, n, X, ldx, stride_x, Y, ldy, stride_y, nrhs, K, ldk, stride_k, Dinv,
+                          stride_dinv, nullptr, 0, 0, alpha, stride_alpha, info, ws, ws_bytes);
+}
+
+gpx_status gpx_fit_batched_params_f64(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n,
+                                      const double* X, int64_t ldx, int64_t stride_x, const double* Y, int64_t ldy,
+                                      int64_t stride_y, int64_t nrhs, double* K, int64_t ldk, int64_t stride_k,
+                                      double* Dinv, int64_t stride_dinv, double* W, int64_t ldw, int64_t stride_w,
+                                      double* alpha, int64_t stride_alpha, int32_t* info, void* ws, size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  GPX_NONNULL(c, W);
+  return fit_batched_impl(h, p, 1, batch, n, X, ldx, stride_x, Y, ldy, stride_y, nrhs, K, ldk, stride_k, Dinv,
+                          stride_dinv, W, ldw, stride_w, alpha, stride_alpha, info, ws, ws_bytes);
+}
+
+gpx_status gpx_fit_factor_batched_params_f64(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n,
+                                             const double* X, int64_t ldx, int64_t stride_x, const double* Y,
+                                             int64_t ldy, int64_t stride_y, int64_t nrhs, double* K, int64_t ldk,
+                                             int64_t stride_k, double* Dinv, int64_t stride_dinv, double* alpha,
+                                             int64_t stride_alpha, int32_t* info, void* ws, size_t ws_bytes) {
+  return fit_batched_impl(h, p, 1, batch, n, X, ldx, stride_x, Y, ldy, stride_y, nrhs, K, ldk, stride_k, Dinv,
                           stride_dinv, nullptr, 0, 0, alpha, stride_alpha, info, ws, ws_bytes);
 }
 
@@ -720,6 +775,49 @@ gpx_status gpx_mll_grad_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n,
   GPX_USE_DEVICE(c);
   return hip_check(c, gpx::launch_mll(c, *p, (int)n, (int)npad, X, ldx, Y, ldy, (int)nrhs, L, ldl, W, ldw, alpha, out,
                                       align256(ws)), "mll");
+}
+
+// T independent problems (one gpx_kernel_params each): the fitted state of problem b at base + b * stride_*, out at
+// out + b * GPX_MLL_NOUT.  One gradient pass per problem on the stream, the workspace of gpx_mll_workspace_size reused by
+// each (the pass fills the GPU from n ~ 1000 on; the per-problem parameters enter the contraction's dK/dtheta epilogue).
+gpx_status gpx_mll_grad_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n, const double* X,
+                                    int64_t ldx, int64_t stride_x, const double* Y, int64_t ldy, int64_t stride_y,
+                                    int64_t nrhs, const double* L, int64_t ldl, int64_t stride_l, const double* W,
+                                    int64_t ldw, int64_t stride_w, const double* alpha, int64_t stride_alpha,
+                                    double* out, void* ws, size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  if (batch < 1 || batch > 65535) return fail(c, GPX_INVALID_ARG, "batch must be in [1, 65535]");
+  GPX_NONNULL(c, p);
+  for (int64_t b = 0; b < batch; ++b) {
+    const gpx_status st = check_params(c, p + b);
+    if (st != GPX_OK) return fail(c, st, "problem " + std::to_string(b) + ": " + c->last_error);
+  }
+  GPX_TRY(check_n(c, n));
+  GPX_NONNULL(c, X);
+  GPX_NONNULL(c, Y);
+  GPX_NONNULL(c, L);
+  GPX_NONNULL(c, W);
+  GPX_NONNULL(c, alpha);
+  GPX_NONNULL(c, out);
+  GPX_NONNULL(c, ws);
+  const int64_t npad = padded(n);
+  for (int64_t b = 0; b < batch; ++b) GPX_TRY(check_ld(c, ldx, p[b].d, "X", false));
+  GPX_TRY(check_ld(c, ldl, npad, "L", false));
+  GPX_TRY(check_ld(c, ldw, npad, "W", true));
+  if (nrhs < 1 || nrhs > GPX_MAX_RHS) return fail(c, GPX_INVALID_ARG, "nrhs must be in [1, 8]");
+  GPX_TRY(check_ld(c, ldy, nrhs, "Y", false));
+  if (batch > 1 && (stride_x < 0 || stride_y < 0 || stride_l < npad * ldl || stride_w < npad * ldw ||
+                    stride_alpha < npad * nrhs))
+    return fail(c, GPX_INVALID_ARG, "batch strides smaller than one problem (X / Y: >= 0)");
+  if (ws_bytes < gpx::mll_workspace_bytes(npad) + 256) return fail(c, GPX_INVALID_ARG, "mll workspace too small");
+  GPX_USE_DEVICE(c);
+  for (int64_t b = 0; b < batch; ++b)
+    GPX_TRY(hip_check(c, gpx::launch_mll(c, p[b], (int)n, (int)npad, X + b * stride_x, ldx, Y + b * stride_y, ldy,
+                                         (int)nrhs, L + b * stride_l, ldl, W + b * stride_w, ldw, alpha + b * stride_alpha,
+                                         out + b * GPX_MLL_NOUT, align256(ws)),
+                      "mll"));
+  return GPX_OK;
 }
 
 gpx_status gpx_moments_grad_workspace_size(int64_t n, int64_t m, size_t* bytes) {
@@ -853,6 +951,87 @@ gpx_status gpx_acquire_argmax_f64(gpx_handle h, const gpx_kernel_params* p, int6
                                               mc, b, 1, a, nullptr, nullptr, nullptr, 0, nullptr,
                                               scores_out ? scores_out + s : nullptr, rec, index_offset + s),
                       "acquire"));
+    rec += (mc + 255) / 256;
+  }
+  return hip_check(c, gpx::launch_argmax_final(c, b.rec_val, b.rec_idx, rec, best_val, best_idx), "argmax");
+}
+
+gpx_status gpx_sweep_multi_workspace_size(int64_t n, int64_t m, size_t* bytes) {
+  if (!bytes || n < 1 || m < 1) return GPX_INVALID_ARG;
+  const int64_t npad = padded(n);
+  *bytes = ((gpx::sweep_workspace_bytes(npad, 1, m) + 255) & ~(size_t)255) +
+           2 * (size_t)gpx::sweep_chunk_size(npad, m) * sizeof(double) + 256;
+  return GPX_OK;
+}
+
+gpx_status gpx_acquire_argmax_multi_f64(gpx_handle h, const gpx_kernel_params* p, int64_t T, int64_t n, const double* X,
+                                        int64_t ldx, const double* const* W_host, const int64_t* ldw_host,
+                                        const double* const* alpha_host, const double* weights_host,
+                                        const double* y_mean_host, const double* y_scale_host, const double* Xs,
+                                        int64_t m, int64_t ldxs, const gpx_acq_params* a, int64_t index_offset,
+                                        double* best_val, int64_t* best_idx, double* scores_out, void* ws,
+                                        size_t ws_bytes) {
+  Context* c = reinterpret_cast<Context*>(h);
+  if (!c) return GPX_INVALID_ARG;
+  if (T < 1 || T > 64) return fail(c, GPX_INVALID_ARG, "T (outputs) must be in [1, 64]");
+  GPX_NONNULL(c, p);
+  GPX_NONNULL(c, weights_host);
+  for (int64_t t = 0; t < T; ++t) {
+    const gpx_status st = check_params(c, p + t);
+    if (st != GPX_OK) return fail(c, st, "output " + std::to_string(t) + ": " + c->last_error);
+    if (p[t].d != p[0].d) return fail(c, GPX_INVALID_ARG, "every output needs the same input dimension d");
+    if (!std::isfinite(weights_host[t])) return fail(c, GPX_INVALID_ARG, "objective weights must be finite");
+    if (y_scale_host && !(y_scale_host[t] > 0.0)) return fail(c, GPX_INVALID_ARG, "y_scale must be positive");
+  }
+  GPX_TRY(check_n(c, n));
+  if (m < 1) return fail(c, GPX_INVALID_ARG, "m must be >= 1");
+  if (!a) return fail(c, GPX_INVALID_ARG, "acquisition params pointer is NULL");
+  if (a->kind < GPX_ACQ_EI || a->kind > GPX_ACQ_VARIANCE) return fail(c, GPX_INVALID_ARG, "unknown acquisition kind");
+  if (a->reserved != 0) return fail(c, GPX_INVALID_ARG, "gpx_acq_params.reserved must be 0");
+  if (a->kind == GPX_ACQ_UCB && !(a->beta >= 0.0)) return fail(c, GPX_INVALID_ARG, "UCB beta must be >= 0");
+  if (index_offset < 0) return fail(c, GPX_INVALID_ARG, "index_offset must be >= 0");
+  GPX_NONNULL(c, X);
+  GPX_NONNULL(c, W_host);
+  GPX_NONNULL(c, ldw_host);
+  GPX_NONNULL(c, alpha_host);
+  GPX_NONNULL(c, Xs);
+  GPX_NONNULL(c, best_val);
+  GPX_NONNULL(c, best_idx);
+  GPX_NONNULL(c, ws);
+  const int64_t npad = padded(n);
+  GPX_TRY(check_ld(c, ldx, p->d, "X", false));
+  GPX_TRY(check_ld(c, ldxs, p->d, "Xs", false));
+  for (int64_t t = 0; t < T; ++t) {
+    if (!W_host[t] || !alpha_host[t]) return fail(c, GPX_INVALID_ARG, "W / alpha of output " + std::to_string(t) + " is NULL");
+    GPX_TRY(check_ld(c, ldw_host[t], npad, "W", true));
+  }
+  size_t need = 0;
+  GPX_TRY(gpx_sweep_multi_workspace_size(n, m, &need));
+  if (ws_bytes < need) return fail(c, GPX_INVALID_ARG, "multi-output sweep workspace too small");
+  gpx::SweepBuffers b;
+  const size_t sweep_bytes = (gpx::sweep_workspace_bytes(npad, 1, m) + 255) & ~(size_t)255;
+  GPX_TRY(carve_sweep(c, npad, 1, m, ws, sweep_bytes, &b));
+  GPX_USE_DEVICE(c);
+  gpx::MultiOutput mo;
+  mo.acc_mu = reinterpret_cast<double*>(reinterpret_cast<char*>(align256(ws)) + sweep_bytes);
+  mo.acc_var = mo.acc_mu + b.chunk;
+  int64_t rec = 0;
+  for (int64_t s = 0; s < m; s += b.chunk) {
+    const int64_t mc = (m - s) < b.chunk ? (m - s) : b.chunk;
+    for (int64_t t = 0; t < T; ++t) {
+      mo.weight = weights_host[t];
+      mo.y_mean = y_mean_host ? y_mean_host[t] : 0.0;
+      mo.y_scale = y_scale_host ? y_scale_host[t] : 1.0;
+      mo.first = t == 0;
+      GPX_TRY(hip_check(c,
+                        gpx::launch_sweep_chunk(c, p[t], (int)n, (int)npad, X, ldx, W_host[t], ldw_host[t],
+                                                alpha_host[t], 1, Xs + s * ldxs, ldxs, mc, b, 1, a, nullptr,
+                                                nullptr, nullptr, 0, nullptr, nullptr, 0, 0, &mo),
+                        "acquire (multi-output)"));
+    }
+    GPX_TRY(hip_check(c, gpx::launch_multi_score(c, mo, *a, mc, scores_out ? scores_out + s : nullptr, b.rec_val + rec,
+                                                 b.rec_idx + rec, index_offset + s),
+                      "acquire (multi-output score)"));
     rec += (mc + 255) / 256;
   }
   return hip_check(c, gpx::launch_argmax_final(c, b.rec_val, b.rec_idx, rec, best_val, best_idx), "argmax");

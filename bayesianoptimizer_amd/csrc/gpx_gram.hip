@@ -17,11 +17,16 @@ template <int DMAX, bool F32, int KIND>
 __global__ void __launch_bounds__(WG) gram_kernel(gpx_kernel_params p, int n, int t0, const double* __restrict__ X,
                                                   int64_t ldx, double* __restrict__ K, int64_t ldk, int64_t sx,
                                                   int64_t sk, int32_t* __restrict__ info,
-                                                  unsigned long long* __restrict__ zero, int64_t zero_words) {
+                                                  unsigned long long* __restrict__ zero, int64_t zero_words,
+                                                  double* __restrict__ mean_out) {
   // the fit's pivot-failure word is cleared here (stream-ordered before the Cholesky) instead of by a separate
   // memset dispatch (~4.7 us at small n), and so are the words of `zero` (the triangular solve's hand-off granules,
-  // gpx_fit_factor_f64): one more dispatch saved
-  if (info && blockIdx.x == 0 && blockIdx.z == 0 && threadIdx.x == 0) info[blockIdx.y] = 0;
+  // gpx_fit_factor_f64): one more dispatch saved.  mean_out (per-problem parameters): the problem's constant mean, read
+  // by the triangular solves of the same fit (Batch::means)
+  if (blockIdx.x == 0 && blockIdx.z == 0 && threadIdx.x == 0) {
+    if (info) info[blockIdx.y] = 0;
+    if (mean_out) mean_out[blockIdx.y] = p.const_mean;
+  }
   if (zero) {
     const int64_t nwg = (int64_t)gridDim.x * gridDim.y * gridDim.z;
     const int64_t wg = blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z);
@@ -125,8 +130,12 @@ template <int DMAX, int KIND>
 __global__ void __launch_bounds__(WG) gram_mfma_kernel(gpx_kernel_params p, int n, int t0, const double* __restrict__ X,
                                                        int64_t ldx, double* __restrict__ K, int64_t ldk, int64_t sx,
                                                        int64_t sk, int32_t* __restrict__ info,
-                                                       unsigned long long* __restrict__ zero, int64_t zero_words) {
-  if (info && blockIdx.x == 0 && blockIdx.z == 0 && threadIdx.x == 0) info[blockIdx.y] = 0;
+                                                       unsigned long long* __restrict__ zero, int64_t zero_words,
+                                                       double* __restrict__ mean_out) {
+  if (blockIdx.x == 0 && blockIdx.z == 0 && threadIdx.x == 0) {
+    if (info) info[blockIdx.y] = 0;
+    if (mean_out) mean_out[blockIdx.y] = p.const_mean;
+  }
   if (zero) {
     const int64_t nwg = (int64_t)gridDim.x * gridDim.y * gridDim.z;
     const int64_t wg = blockIdx.x + (int64_t)gridDim.x * (blockIdx.y + (int64_t)gridDim.y * blockIdx.z);
@@ -213,7 +222,7 @@ __global__ void __launch_bounds__(WG) gram_mfma_kernel(gpx_kernel_params p, int 
 
 hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
                        double* K, int64_t ldk, const Batch& bt, int rb0, int32_t* info, void* zero,
-                       size_t zero_bytes) {
+                       size_t zero_bytes, double* mean_out) {
   LaunchTimer tm(c, GPX_TIMER_GRAM);
   const int nblk = npad / NB;
   const int t0 = rb0 * (rb0 + 1) / 2;  // tiles of the row blocks above rb0 are skipped (gpx_append_f64)
@@ -226,8 +235,9 @@ hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, 
   auto* zp = reinterpret_cast<unsigned long long*>(zero);
   const int64_t zw = zero ? (int64_t)(zero_bytes / 8) : 0;
 #define GPX_GRAM_K(D, KIND)                                                                                      \
-  (p.cov_fp32 ? gram_kernel<D, true, KIND><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info, zp, zw) \
-              : gram_mfma_kernel<D, KIND><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info, zp, zw))
+  (p.cov_fp32 ? gram_kernel<D, true, KIND><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info, zp, zw, mean_out) \
+              : gram_mfma_kernel<D, KIND><<<grid, WG, 0, c->stream>>>(p, n, t0, X, ldx, K, ldk, bt.x, bt.k, info, zp, zw, \
+                                                                 mean_out))
 #define GPX_GRAM(D)                                                                                              \
   (p.kind == GPX_KERNEL_RBF        ? GPX_GRAM_K(D, GPX_KERNEL_RBF)                                               \
    : p.kind == GPX_KERNEL_MATERN52 ? GPX_GRAM_K(D, GPX_KERNEL_MATERN52)                                          \

@@ -76,16 +76,22 @@ struct LaunchTimer {
 // `count` independent problems of the same n / d / kernel parameters (restarts or seeds, BASELINE configs[3]) run in
 // the same launches: the problem index is one more grid dimension and every array of problem b starts at
 // base + b * stride (element strides; a workspace slice of `ws` doubles per problem).  count = 1: a single fit.
+// Read-only inputs (x, y) may use any stride >= 0 (0: every problem reads the same X, e.g. the T outputs of one
+// multi-output model; y = 1 with ldy = T: output column b of one n x T target matrix).  means (device, optional): per-problem
+// constant means written by the fit's Gram launches when the problems carry their own kernel parameters
+// (gpx_fit_*_batched_params_f64); the triangular solves then read means[b] instead of their scalar const_mean.
 struct Batch {
   int count = 1;
   int64_t x = 0, y = 0, k = 0, dinv = 0, w = 0, alpha = 0, ws = 0;
+  const double* means = nullptr;
 };
 
 // ---- launch wrappers (defined in the .hip files) -------------------------------------------------
 // zero / zero_bytes (optional, a multiple of 8): a buffer the Gram launch clears besides (the next launches' flags)
+// mean_out (optional): mean_out[b] = p.const_mean for each problem b of the launch (Batch::means of the solves)
 hipError_t launch_gram(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
                        double* K, int64_t ldk, const Batch& bt = Batch(), int rb0 = 0, int32_t* info = nullptr,
-                       void* zero = nullptr, size_t zero_bytes = 0);
+                       void* zero = nullptr, size_t zero_bytes = 0, double* mean_out = nullptr);
 // The forward half of alpha's triangular solve folded into the dataflow Cholesky: z = L^{-1} (Y - mean), with the
 // padded rows and right-hand sides >= nrhs at 0.  buf (per problem, stride 2 npad nr doubles): the running right-hand
 // sides (npad x nr), then z (npad x nr); nr = 1 for one right-hand side, else GPX_MAX_RHS (potrs' layout).
@@ -94,6 +100,7 @@ struct ForwardRhs {
   int64_t ldy = 0, sy = 0;  // sy: Y stride per problem
   int nrhs = 1, n = 0;
   double mean = 0.0;
+  const double* means = nullptr;  // per-problem means (device), overriding `mean` (Batch::means)
   double* buf = nullptr;
 };
 inline int rhs_row(int nrhs) { return nrhs == 1 ? 1 : GPX_MAX_RHS; }
@@ -130,13 +137,24 @@ struct SweepBuffers {
   int64_t* rec_idx;
   int64_t chunk;     // C
 };
-// mode 0: posterior (write mean/var); mode 1: acquisition (records + optional scores)
+// One output t of a linear objective sum_t w_t f_t over independent GPs (gpx_acquire_argmax_multi_f64): the chunk's
+// posterior of output t, untransformed by (y_mean, y_scale), weighted into chunk-sized accumulators.
+struct MultiOutput {
+  double weight = 1.0, y_mean = 0.0, y_scale = 1.0;
+  int first = 1;
+  double* acc_mu = nullptr;
+  double* acc_var = nullptr;
+};
+// mode 0: posterior (write mean/var); mode 1: acquisition (records + optional scores); mo != nullptr: accumulate one
+// output of a multi-output objective instead (mode ignored), scored afterwards by launch_multi_score
 hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int npad, const double* X, int64_t ldx,
                               const double* W, int64_t ldw, const double* alpha, int nrhs, const double* Xs,
                               int64_t ldxs, int64_t m_chunk, const SweepBuffers& b, int mode,
                               const gpx_acq_params* a, const double* y_mean, const double* y_scale,
                               double* mean_out, int64_t ldmean, double* var_out, double* scores_out,
-                              int64_t rec_offset, int64_t index_offset);
+                              int64_t rec_offset, int64_t index_offset, const MultiOutput* mo = nullptr);
+hipError_t launch_multi_score(Context* c, const MultiOutput& mo, const gpx_acq_params& a, int64_t m_chunk,
+                              double* scores_out, double* rec_val, int64_t* rec_idx, int64_t index_offset);
 hipError_t launch_argmax_final(Context* c, const double* vals, const int64_t* idx, int64_t count, double* best_val,
                                int64_t* best_idx);
 // the cross-GPU exchange (gpx_comm.cpp): pack the device record into {double value; int64 index}, and reduce

@@ -59,6 +59,9 @@ static_assert(NB * LD64 + DBUF >= Tile64::LDS_DOUBLES && DBUF >= 2 * 16 * LDD, "
 constexpr int PANEL_LDS = 2 * NB * LD64 + DBUF + NB * GPX_MAX_RHS;
 constexpr int STEP_LDS = PANEL_LDS > Tile128::LDS_DOUBLES ? PANEL_LDS : Tile128::LDS_DOUBLES;
 static_assert(STEP_LDS * 8 + 64 <= 81920, "two workgroups per CU");
+// the 128 x 128 trailing tiles run the hand-placed k loop (gpx_trmm_asm.h) on the step kernel's LDS buffer
+static_assert(Tile128::LDS_DOUBLES * 8 == trmm_asm::LDS_BYTES && STEP_LDS >= Tile128::LDS_DOUBLES,
+              "hand-placed tile uses MfmaTile's LDS image and needs the step kernel's buffer to hold it");
 
 // C - L_a L_b^T for a 64x64 tile into the LDS tile S (row length LD64): acc seeded with -C (its loads issued with the
 // first k-tile's, no load round trip after the product), acc += L_a L_b^T over K, S = -acc.
@@ -144,6 +147,7 @@ struct PotrfFwd {
   int64_t sb = 0;           // r / z stride per problem
   int nrhs = 1, n = 0;
   double mean = 0.0;
+  const double* means = nullptr;  // per-problem constant means (device): mean = means[problem]
 };
 
 __device__ __forceinline__ double fwd_y(const PotrfFwd& f, int row, int rr) {
@@ -823,6 +827,7 @@ potrf_step_kernel(double* __restrict__ A, int64_t lda, int c, int nblk, StepPlan
   if (role == 0) {
     if constexpr (NR > 0) {
       f.Y += blockIdx.y * f.sy;
+      if (f.means) f.mean = f.means[blockIdx.y];
       f.r += blockIdx.y * f.sb;
       f.z += blockIdx.y * f.sb;
     }
@@ -1029,6 +1034,7 @@ hipError_t launch_potrf(Context* ctx, int npad, double* A, int64_t lda, double* 
     f.nrhs = fr->nrhs;
     f.n = fr->n;
     f.mean = fr->mean;
+    f.means = fr->means;
   }
   launch_steps(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, f);
   launch_dinv(ctx, nblk, A, lda, Dinv, info, bt, 0, nblk, W, ldw);

@@ -697,8 +697,9 @@ __global__ void __launch_bounds__(WG) potrs_kernel(int n, int npad, const double
                                                    int32_t* __restrict__ info, unsigned long long* granules,
                                                    unsigned* abort_ptr, int64_t sl, int64_t sd, int64_t sy, int64_t sa,
                                                    int64_t sg, unsigned limit, const double* __restrict__ zin,
-                                                   int64_t sz) {
+                                                   int64_t sz, const double* __restrict__ means) {
   const int prob = blockIdx.y;
+  if (means) const_mean = means[prob];  // per-problem kernel parameters (Batch::means)
   if (zin) zin += prob * sz;
   L += prob * sl;
   Dinv += prob * sd;
@@ -767,12 +768,12 @@ hipError_t launch_potrs(Context* c, int n, int npad, const double* L, int64_t ld
   if (nrhs == 1)
     potrs_kernel<1><<<dim3(G, bt.count), WG, 0, c->stream>>>(n, npad, L, ldl, Dinv, Y, ldy, nrhs, const_mean, alpha,
                                                              info, granules, abort_word, bt.k, bt.dinv, bt.y,
-                                                             bt.alpha, sg, c->spin_limit, z, sz);
+                                                             bt.alpha, sg, c->spin_limit, z, sz, bt.means);
   else
     potrs_kernel<GPX_MAX_RHS><<<dim3(G, bt.count), WG, 0, c->stream>>>(n, npad, L, ldl, Dinv, Y, ldy, nrhs,
                                                                        const_mean, alpha, info, granules, abort_word,
                                                                        bt.k, bt.dinv, bt.y, bt.alpha, sg, c->spin_limit,
-                                                                       z, sz);
+                                                                       z, sz, bt.means);
   return hipGetLastError();
 }
 

@@ -502,8 +502,17 @@ struct FinalizeArgs {
   double y_scale[GPX_MAX_RHS];
   int acq_kind;
   double best_f, beta;
+  // modes 2 / 3: a linear objective sum_t w_t f_t over T independent GPs (gpx_acquire_argmax_multi_f64)
+  double weight;     // mode 2: w_t of this output
+  int first;         // mode 2: the first output of the chunk (overwrites the accumulators)
+  double* acc_mu;    // sum_t w_t (y_mean_t + y_scale_t mu_t)                 (chunk-sized)
+  double* acc_var;   // sum_t w_t^2 y_scale_t^2 max(k** - |v_t|^2, 1e-10)      (chunk-sized)
 };
 
+// mode 0: posterior (mean / variance out); 1: acquisition + 256-candidate block argmax; 2: one output of a multi-output
+// objective into the accumulators; 3: acquisition + block argmax of the accumulated objective (no partials read).
+// Variance floors: GPyTorch's 1e-10 per output in the standardised space, BoTorch's 1e-12 on the scored variance
+// [upstream] (T = 1, w = 1: modes 2 + 3 give mode 1's value bit for bit).
 __global__ void __launch_bounds__(WG) finalize_kernel(FinalizeArgs fa, int mode, const double* __restrict__ Xs,
                                                       int64_t ldxs, int64_t m_chunk, int64_t C, int nrhs, int nJB,
                                                       int nI, const double* __restrict__ mu_part,
@@ -517,35 +526,48 @@ __global__ void __launch_bounds__(WG) finalize_kernel(FinalizeArgs fa, int mode,
   const bool valid = c < m_chunk;
   double score = -INFINITY;
   if (valid) {
-    // prior variance k(x, x)
-    double kd = p.outputscale;
-    if (p.kind == GPX_KERNEL_SCALE_LINEAR_MATERN52) {
-      double lv = 0.0;
-      for (int k = 0; k < p.d; ++k) {
-        const double v = Xs[c * ldxs + k];
-        lv += v * v * p.linear_variance[k];
+    double mu, var;
+    if (mode == 3) {
+      mu = fa.acc_mu[c];
+      var = fmax(fa.acc_var[c], 1e-12);
+    } else {
+      // prior variance k(x, x)
+      double kd = p.outputscale;
+      if (p.kind == GPX_KERNEL_SCALE_LINEAR_MATERN52) {
+        double lv = 0.0;
+        for (int k = 0; k < p.d; ++k) {
+          const double v = Xs[c * ldxs + k];
+          lv += v * v * p.linear_variance[k];
+        }
+        kd = p.outputscale * (lv + 1.0);
       }
-      kd = p.outputscale * (lv + 1.0);
-    }
-    const double ss = sum_partials(ss_part + c, nI, C);
-    double var = fmax(kd - ss, 1e-10);  // gpytorch min_variance (float64) [upstream]
-    if (mode == 0) {
-      for (int q = 0; q < nrhs; ++q) {
-        double mu = sum_partials(mu_part + (int64_t)q * C + c, nJB, (int64_t)nrhs * C);
-        mu += p.const_mean;
-        mean_out[c * ldmean + q] = fa.y_mean[q] + fa.y_scale[q] * mu;
+      const double ss = sum_partials(ss_part + c, nI, C);
+      var = fmax(kd - ss, 1e-10);  // gpytorch min_variance (float64) [upstream]
+      if (mode == 0) {
+        for (int q = 0; q < nrhs; ++q) {
+          double mq = sum_partials(mu_part + (int64_t)q * C + c, nJB, (int64_t)nrhs * C);
+          mq += p.const_mean;
+          mean_out[c * ldmean + q] = fa.y_mean[q] + fa.y_scale[q] * mq;
+        }
+        var_out[c] = fmax(var * (fa.y_scale[0] * fa.y_scale[0]), 1e-12);  // BoTorch min_var [upstream]
+        return;
       }
-      var_out[c] = fmax(var * (fa.y_scale[0] * fa.y_scale[0]), 1e-12);  // BoTorch min_var [upstream]
-      return;
+      mu = sum_partials(mu_part + c, nJB, C);
+      mu = fa.y_mean[0] + fa.y_scale[0] * (mu + p.const_mean);
+      var = var * (fa.y_scale[0] * fa.y_scale[0]);
+      if (mode == 2) {
+        const double wm = fa.weight * mu, wv = (fa.weight * fa.weight) * var;
+        fa.acc_mu[c] = fa.first ? wm : fa.acc_mu[c] + wm;
+        fa.acc_var[c] = fa.first ? wv : fa.acc_var[c] + wv;
+        return;
+      }
+      var = fmax(var, 1e-12);
     }
-    double mu = sum_partials(mu_part + c, nJB, C);
-    mu = fa.y_mean[0] + fa.y_scale[0] * (mu + p.const_mean);
-    var = fmax(var * (fa.y_scale[0] * fa.y_scale[0]), 1e-12);
     score = acq_score(fa.acq_kind, mu, var, fa.best_f, fa.beta);
     if (scores_out) scores_out[c] = score;
     if (score != score) score = -INFINITY;
   }
-  if (mode == 0) return;
+  if (mode == 0 || mode == 2) return;
   // block argmax
   double bv = score;
   int64_t bi = valid ? index_base + c : INT64_MAX;
@@ -645,7 +667,7 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
                               int64_t ldxs, int64_t m_chunk, const SweepBuffers& b, int mode,
                               const gpx_acq_params* a, const double* y_mean, const double* y_scale,
                               double* mean_out, int64_t ldmean, double* var_out, double* scores_out,
-                              int64_t rec_offset, int64_t index_offset) {
+                              int64_t rec_offset, int64_t index_offset, const MultiOutput* mo) {
   const int64_t C = b.chunk;
   int nJB = npad / NB, nI = npad / TT;
   const int ncb = (int)((m_chunk + WG - 1) / WG);  // 256-candidate blocks actually used in this chunk
@@ -728,11 +750,38 @@ hipError_t launch_sweep_chunk(Context* c, const gpx_kernel_params& p, int n, int
       fa.y_mean[0] = a->y_mean;
       fa.y_scale[0] = a->y_scale;
     }
+    fa.weight = 1.0;
+    fa.first = 0;
+    fa.acc_mu = fa.acc_var = nullptr;
+    if (mo) {  // one output of a multi-output objective: accumulate, score later (launch_multi_score)
+      mode = 2;
+      fa.y_mean[0] = mo->y_mean;
+      fa.y_scale[0] = mo->y_scale;
+      fa.weight = mo->weight;
+      fa.first = mo->first;
+      fa.acc_mu = mo->acc_mu;
+      fa.acc_var = mo->acc_var;
+    }
     finalize_kernel<<<ncb, WG, 0, c->stream>>>(fa, mode, Xs, ldxs, m_chunk, C, nrhs, nJB, nI, b.mu_part,
                                                    b.ss_part, mean_out, ldmean, var_out, scores_out,
                                                    b.rec_val + rec_offset, b.rec_idx + rec_offset,
                                                    index_offset);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_multi_score(Context* c, const MultiOutput& mo, const gpx_acq_params& a, int64_t m_chunk,
+                              double* scores_out, double* rec_val, int64_t* rec_idx, int64_t index_offset) {
+  LaunchTimer tm(c, GPX_TIMER_ACQ);
+  FinalizeArgs fa{};
+  fa.acq_kind = a.kind;
+  fa.best_f = a.best_f;
+  fa.beta = a.beta;
+  fa.acc_mu = mo.acc_mu;
+  fa.acc_var = mo.acc_var;
+  const int ncb = (int)((m_chunk + WG - 1) / WG);
+  finalize_kernel<<<ncb, WG, 0, c->stream>>>(fa, 3, nullptr, 0, m_chunk, 0, 1, 0, 0, nullptr, nullptr, nullptr, 0,
+                                             nullptr, scores_out, rec_val, rec_idx, index_offset);
   return hipGetLastError();
 }
 

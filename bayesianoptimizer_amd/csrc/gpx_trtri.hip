@@ -232,7 +232,8 @@ constexpr int AK = 128;  // k-chunk of the z = W^T y pass
 __global__ void __launch_bounds__(WG) alpha_z_kernel(int n, int npad, const double* __restrict__ W, int64_t ldw,
                                                      const double* __restrict__ Y, int64_t ldy, int nrhs,
                                                      double const_mean, double* __restrict__ zpart, int64_t sw,
-                                                     int64_t sy, int64_t sws) {
+                                                     int64_t sy, int64_t sws, const double* __restrict__ means) {
+  if (means) const_mean = means[blockIdx.z];  // per-problem kernel parameters (Batch::means)
   W += blockIdx.z * sw;  // problem of a batched fit
   Y += blockIdx.z * sy;
   zpart += blockIdx.z * sws;
@@ -336,7 +337,8 @@ hipError_t launch_alpha(Context* c, int n, int npad, const double* W, int64_t ld
                         int nrhs, double const_mean, double* alpha, double* zpart, double* z, const Batch& bt) {
   LaunchTimer tm(c, GPX_TIMER_ALPHA);
   dim3 g1((npad + WG - 1) / WG, npad / AK, bt.count);
-  alpha_z_kernel<<<g1, WG, 0, c->stream>>>(n, npad, W, ldw, Y, ldy, nrhs, const_mean, zpart, bt.w, bt.y, bt.ws);
+  alpha_z_kernel<<<g1, WG, 0, c->stream>>>(n, npad, W, ldw, Y, ldy, nrhs, const_mean, zpart, bt.w, bt.y, bt.ws,
+                                              bt.means);
   if (npad <= 4 * AK) {  // <= 4 chunks: alpha_w sums them itself (z entries re-read per row, from L2)
     alpha_w_kernel<<<dim3((npad + 3) / 4, bt.count), WG, 0, c->stream>>>(n, npad, W, ldw, zpart, nrhs, alpha, bt.w,
                                                                           bt.ws, bt.alpha, 1);

@@ -385,13 +385,14 @@ class GPEngine:
             state.check()
         return state
 
-    def fit_batched(self, X, Y, params: KernelParams, check: bool = True,
+    def fit_batched(self, X, Y, params: Union[KernelParams, Sequence[KernelParams]], check: bool = True,
                     out: Optional[Sequence[GPState]] = None, inverse: bool = False) -> list:
-        """Posterior updates of B independent problems (X: B x n x d, Y: B x n or B x n x nrhs) sharing n, d and the
-        hyperparameters (restarts / seeds, BASELINE configs[3]) in the same launches (gpx_fit_factor_batched_f64, or
-        gpx_fit_batched_f64 with ``inverse``: W formed for every problem in the same launches).  Returns one GPState per
-        problem (views into stacked device tensors); results equal B calls of ``fit``.  With ``check`` synchronises and
-        raises NotPositiveDefiniteError for the first failing problem."""
+        """Posterior updates of B independent problems (X: B x n x d, Y: B x n or B x n x nrhs) sharing n and d
+        (restarts / seeds, BASELINE configs[3]) in the same launches (gpx_fit_factor_batched_f64, or gpx_fit_batched_f64
+        with ``inverse``: W formed for every problem in the same launches).  ``params``: one KernelParams shared by all
+        problems, or a sequence of B (gpx_fit_*_batched_params_f64).  Returns one GPState per problem (views into
+        stacked device tensors); results equal B calls of ``fit``.  With ``check`` synchronises and raises
+        NotPositiveDefiniteError for the first failing problem."""
         X = X if isinstance(X, torch.Tensor) else torch.as_tensor(X)
         Y = Y if isinstance(Y, torch.Tensor) else torch.as_tensor(Y)
         X = X.to(device=self.device, dtype=torch.float64).contiguous()
@@ -404,10 +405,44 @@ class GPEngine:
         B, n, d = X.shape
         if Y.shape[:2] != (B, n):
             raise ValueError(f"Y must be {B} x {n} (x nrhs), got {tuple(Y.shape)}")
-        nrhs = Y.shape[2]
+        return self._fit_batch(X, X.stride(1), X.stride(0), Y, Y.stride(1), Y.stride(0), Y.shape[2], B, n, d, params,
+                               check, out, inverse, [X[b] for b in range(B)])
+
+    def fit_outputs(self, X, Y, params: Sequence[KernelParams], check: bool = True,
+                    out: Optional[Sequence[GPState]] = None, inverse: bool = False) -> list:
+        """T independent GPs on ONE training set: X n x d, Y n x T, one KernelParams per output — the reference's
+        multi-output SingleTaskGP (optimization/Bayesian1.py:108-116: a batch of independent GPs on one X, each with its
+        own lengthscales, outputscale, noise and constant mean [upstream]).  One call of gpx_fit_*_batched_params_f64
+        with X shared (stride 0) and Y read column by column (stride 1, ldy = T): the Cholesky and solves of all T
+        outputs run in the same launches.  Returns one GPState per output (nrhs = 1, X = the shared tensor)."""
+        X = self._as_f64(X, "X")
+        Y = self._as_f64(Y, "Y")
+        n, d = X.shape
+        if Y.shape[0] != n:
+            raise ValueError(f"X has {n} rows but Y has {Y.shape[0]}")
+        T = Y.shape[1]
+        if len(params) != T:
+            raise ValueError(f"expected {T} kernel parameter sets (one per output), got {len(params)}")
+        return self._fit_batch(X, X.stride(0), 0, Y, Y.stride(0), 1, 1, T, n, d, list(params), check, out, inverse,
+                               [X] * T)
+
+    @staticmethod
+    def batch_info(states: Sequence[GPState]):
+        """The pivot-failure words of ``states`` as one host array (one synchronisation): 0, pivot + 1, or
+        GPX_INFO_TIMEOUT."""
+        b0 = states[0]._batch
+        if b0 is not None and all(st._batch is b0 for st in states) and b0[4].numel() == len(states):
+            return b0[4].cpu().numpy()
+        return torch.cat([st.info for st in states]).cpu().numpy()
+
+    def _fit_batch(self, X, ldx, sx, Y, ldy, sy, nrhs, B, n, d, params, check, out, inverse, Xviews) -> list:
         if not 1 <= nrhs <= _capi.GPX_MAX_RHS:
             raise ValueError(f"number of outputs {nrhs} outside [1, {_capi.GPX_MAX_RHS}]")
-        pc = params.to_c(d)
+        per_problem = not isinstance(params, KernelParams)
+        plist = list(params) if per_problem else [params] * B
+        if len(plist) != B:
+            raise ValueError(f"expected {B} kernel parameter sets, got {len(plist)}")
+        pcs = (KernelParamsC * B)(*[pp.to_c(d) for pp in plist]) if per_problem else plist[0].to_c(d)
         npad = self.padded_n(n)
         nblk = npad // 64
         if out is not None and len(out) == B and all(s.n == n and s.nrhs == nrhs for s in out) and \
@@ -422,24 +457,26 @@ class GPEngine:
             Ib = torch.zeros((B,), dtype=torch.int32, device=dev)
         nbytes = ctypes.c_size_t()
         self._bind_stream()
+        pref = pcs if per_problem else ctypes.byref(pcs)
+        sfx = "_params" if per_problem else ""
         if inverse:
             self._check(self.lib.gpx_fit_batched_workspace_size(n, nrhs, B, ctypes.byref(nbytes)))
             ws = self.workspace("fit_batched", nbytes.value)
-            self._check(self.lib.gpx_fit_batched_f64(
-                self.handle, ctypes.byref(pc), B, n, _ptr(X), X.stride(1), X.stride(0), _ptr(Y), Y.stride(1),
-                Y.stride(0), nrhs, _ptr(Lb), npad, Lb.stride(0), _ptr(Db), Db.stride(0), _ptr(Wb), npad, Wb.stride(0),
-                _ptr(Ab), Ab.stride(0), _ptr(Ib), _ptr(ws), ws.numel()))
+            self._check(getattr(self.lib, f"gpx_fit_batched{sfx}_f64")(
+                self.handle, pref, B, n, _ptr(X), ldx, sx, _ptr(Y), ldy, sy, nrhs, _ptr(Lb), npad, Lb.stride(0),
+                _ptr(Db), Db.stride(0), _ptr(Wb), npad, Wb.stride(0), _ptr(Ab), Ab.stride(0), _ptr(Ib), _ptr(ws),
+                ws.numel()))
         else:
             self._check(self.lib.gpx_fit_factor_batched_workspace_size(n, nrhs, B, ctypes.byref(nbytes)))
             ws = self.workspace("potrs_batched", nbytes.value)
-            self._check(self.lib.gpx_fit_factor_batched_f64(
-                self.handle, ctypes.byref(pc), B, n, _ptr(X), X.stride(1), X.stride(0), _ptr(Y), Y.stride(1),
-                Y.stride(0), nrhs, _ptr(Lb), npad, Lb.stride(0), _ptr(Db), Db.stride(0), _ptr(Ab), Ab.stride(0),
-                _ptr(Ib), _ptr(ws), ws.numel()))
+            self._check(getattr(self.lib, f"gpx_fit_factor_batched{sfx}_f64")(
+                self.handle, pref, B, n, _ptr(X), ldx, sx, _ptr(Y), ldy, sy, nrhs, _ptr(Lb), npad, Lb.stride(0),
+                _ptr(Db), Db.stride(0), _ptr(Ab), Ab.stride(0), _ptr(Ib), _ptr(ws), ws.numel()))
         states = []
+        batch = (Lb, Wb, Db, Ab, Ib)  # ONE object shared by the states: inverse_batched / batch_info test identity
         for b in range(B):
-            states.append(GPState(X=X[b], L=Lb[b], W=Wb[b], Dinv=Db[b], alpha=Ab[b], info=Ib[b:b + 1], params=params,
-                                  n=n, npad=npad, nrhs=nrhs, _batch=(Lb, Wb, Db, Ab, Ib), W_ready=inverse))
+            states.append(GPState(X=Xviews[b], L=Lb[b], W=Wb[b], Dinv=Db[b], alpha=Ab[b], info=Ib[b:b + 1],
+                                  params=plist[b], n=n, npad=npad, nrhs=nrhs, _batch=batch, W_ready=inverse))
         if check:
             bad = Ib.cpu().numpy()
             for b in range(B):
@@ -541,6 +578,57 @@ class GPEngine:
             return best_val, best_idx, scores
         return best_val, best_idx
 
+    def acquire_multi(self, states: Sequence[GPState], Xs, kind: Union[str, int] = "logei", best_f: float = 0.0,
+                      beta: float = 4.0, weights: Optional[Sequence[float]] = None,
+                      y_mean: Optional[Sequence[float]] = None, y_scale: Optional[Sequence[float]] = None,
+                      index_offset: int = 0, return_scores: bool = False):
+        """Score a linear objective sum_t w_t f_t over the T independent outputs of one ``fit_outputs`` call
+        (gpx_acquire_argmax_multi_f64: mean sum_t w_t (y_mean_t + y_scale_t mu_t), variance sum_t w_t^2 y_scale_t^2
+        var_t) and return device scalars (best_value, best_index) (+ scores).  ``kind="variance"`` with unit weights is
+        the variance-sum pool-scan score (optimization/Bayesian7.py:671)."""
+        Xs = self._as_f64(Xs, "Xs")
+        T = len(states)
+        if T < 1:
+            raise ValueError("no outputs to score")
+        st0 = states[0]
+        if any(st.n != st0.n or st.X.shape != st0.X.shape for st in states):
+            raise ValueError("acquire_multi needs outputs fitted on the same training inputs")
+        d = st0.d
+        if Xs.shape[1] != d:
+            raise ValueError(f"Xs has {Xs.shape[1]} columns, model has d={d}")
+        m = Xs.shape[0]
+        if m == 0:
+            raise ValueError("empty candidate set")
+        self.inverse_batched(states)
+        w = [1.0] * T if weights is None else [float(v) for v in weights]
+        if len(w) != T:
+            raise ValueError(f"expected {T} objective weights, got {len(w)}")
+        ym = [0.0] * T if y_mean is None else [float(v) for v in y_mean]
+        ys = [1.0] * T if y_scale is None else [float(v) for v in y_scale]
+        kid = ACQ_KINDS[kind.lower()] if isinstance(kind, str) else int(kind)
+        ap = AcqParamsC()
+        ap.kind, ap.best_f, ap.beta, ap.y_mean, ap.y_scale = kid, float(best_f), float(beta), 0.0, 1.0
+        pcs = (KernelParamsC * T)(*[st.params.to_c(d) for st in states])
+        best_val = torch.empty((1,), dtype=torch.float64, device=self.device)
+        best_idx = torch.empty((1,), dtype=torch.int64, device=self.device)
+        scores = torch.empty((m,), dtype=torch.float64, device=self.device) if return_scores else None
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_sweep_multi_workspace_size(states[0].n, m, ctypes.byref(nbytes)))
+        ws = self.workspace("sweep_multi", nbytes.value)
+        X = st0.X
+        alphas = [st.alpha[:, 0].contiguous() for st in states]  # keeps the columns alive across the call
+        wp = (ctypes.c_void_p * T)(*[st.W.data_ptr() for st in states])
+        ldw = (ctypes.c_int64 * T)(*[st.W.stride(0) for st in states])
+        ap_ = (ctypes.c_void_p * T)(*[a.data_ptr() for a in alphas])
+        self._bind_stream()
+        self._check(self.lib.gpx_acquire_argmax_multi_f64(
+            self.handle, pcs, T, st0.n, _ptr(X), X.stride(0), wp, ldw, ap_, (ctypes.c_double * T)(*w), (ctypes.c_double * T)(*ym), (ctypes.c_double * T)(*ys), _ptr(Xs),
+            m, Xs.stride(0), ctypes.byref(ap), int(index_offset), _ptr(best_val), _ptr(best_idx), _ptr(scores),
+            _ptr(ws), ws.numel()))
+        if return_scores:
+            return best_val, best_idx, scores
+        return best_val, best_idx
+
     def moments_grad(self, state: GPState, Xs, q: int = 1, alpha: Optional[torch.Tensor] = None):
         """Posterior mean / q-batch covariance of candidates Xs (m x d, consecutive q-batches) and their derivatives
         w.r.t. the candidates (gpx_moments_grad_f64), in the engine's standardised units:
@@ -605,6 +693,73 @@ class GPEngine:
             state.nrhs, _ptr(state.L), state.L.stride(0), _ptr(state.W), state.W.stride(0), _ptr(state.alpha), _ptr(out),
             _ptr(ws), ws.numel()))
         return out
+
+    def mll_grad_outputs(self, states: Sequence[GPState], Y, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """-log p(y_t) and its gradient w.r.t. output t's own hyperparameters for every output of one ``fit_outputs``
+        call (Y: the n x T targets it used), as a T x MLL_NOUT device tensor (gpx_mll_grad_batched_f64).  Asynchronous."""
+        Y = self._as_f64(Y, "Y")
+        T = len(states)
+        st0 = states[0]
+        if Y.shape != (st0.n, T):
+            raise ValueError(f"Y must have shape ({st0.n}, {T}), got {tuple(Y.shape)}")
+        b0 = st0._batch
+        if b0 is None or any(st._batch is not b0 for st in states) or b0[0].shape[0] != T:
+            raise ValueError("mll_grad_outputs needs the states of one fit_outputs call, in order")
+        self.inverse_batched(states)
+        Lb, Wb, Db, Ab, Ib = b0
+        if out is None:
+            out = torch.empty((T, _capi.MLL_NOUT), dtype=torch.float64, device=self.device)
+        nbytes = ctypes.c_size_t()
+        self._check(self.lib.gpx_mll_workspace_size(st0.n, ctypes.byref(nbytes)))
+        ws = self.workspace("mll", nbytes.value)
+        pcs = (KernelParamsC * T)(*[st.params.to_c(st0.d) for st in states])
+        npad = st0.npad
+        self._bind_stream()
+        self._check(self.lib.gpx_mll_grad_batched_f64(
+            self.handle, pcs, T, st0.n, _ptr(st0.X), st0.X.stride(0), 0, _ptr(Y), Y.stride(0), 1, 1, _ptr(Lb), npad,
+            Lb.stride(0), _ptr(Wb), npad, Wb.stride(0), _ptr(Ab), Ab.stride(0), _ptr(out), _ptr(ws), ws.numel()))
+        return out
+
+    def mll_value_grad_outputs(self, X, Y, params: Sequence[KernelParams],
+                               jitters: Sequence[float] = (0.0, 1e-8, 1e-7, 1e-6),
+                               states: Optional[Sequence[GPState]] = None):
+        """``mll_value_grad`` for T independent outputs on one X (Y: n x T, one KernelParams each), all of them in
+        one batched fit + one batched gradient per jitter attempt.  A failing output retries with the next jitter of
+        the ladder while the others keep theirs (psd_safe_cholesky adds jitter only to the failing batch members
+        [upstream]).  Returns (list of T host dicts, states).  Synchronises."""
+        X = self._as_f64(X, "X")
+        Y = self._as_f64(Y, "Y")
+        T = Y.shape[1]
+        level = [0] * T
+        while True:
+            pj = [p.replace(jitter=p.jitter + jitters[level[t]]) for t, p in enumerate(params)]
+            states = self.fit_outputs(X, Y, pj, check=False, out=states, inverse=True)
+            out = self.mll_grad_outputs(states, Y)
+            v = out.cpu().numpy()
+            info = states[0]._batch[4].cpu().numpy()
+            bad = [t for t in range(T) if info[t] != 0]
+            for t in bad:
+                if info[t] < 0:
+                    raise info_error(int(info[t]), f"output {t}")
+            if not bad:
+                break
+            for t in bad:
+                level[t] += 1
+                if level[t] >= len(jitters):
+                    raise NotPositiveDefiniteError(int(info[t]) - 1, f"output {t}: not positive definite at pivot "
+                                                                     f"{int(info[t]) - 1} through the jitter ladder")
+        d = X.shape[1]
+        res = []
+        for t in range(T):
+            r = v[t]
+            res.append({
+                "nll": float(r[_capi.MLL_NLL]), "quad": float(r[_capi.MLL_QUAD]), "logdet": float(r[_capi.MLL_LOGDET]),
+                "noise": float(r[_capi.MLL_D_NOISE]), "outputscale": float(r[_capi.MLL_D_OUTPUTSCALE]),
+                "const_mean": float(r[_capi.MLL_D_MEAN]),
+                "lengthscale": r[_capi.MLL_D_LENGTHSCALE:_capi.MLL_D_LENGTHSCALE + d].copy(),
+                "linear_variance": r[_capi.MLL_D_LINVAR:_capi.MLL_D_LINVAR + d].copy(),
+            })
+        return res, states
 
     def mll_value_grad(self, X, y, params: KernelParams, jitters: Sequence[float] = (0.0, 1e-8, 1e-7, 1e-6),
                        state: Optional[GPState] = None):

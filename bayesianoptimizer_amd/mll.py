@@ -184,36 +184,73 @@ def default_spec(kind: str, d: int, prior_set: str = "dim_scaled", base: Optiona
 
 
 # ---- objective -------------------------------------------------------------------------------------
+def _feasible(spec: HyperSpec, raw) -> bool:
+    """A line-search trial point outside the parameter domain (a softplus underflowing to 0, an overflow) scores +inf,
+    so L-BFGS-B backtracks (GPyTorch's NaN loss plays that role in fit_gpytorch_mll_scipy [upstream])."""
+    nat = [h.to_natural(float(r)) for h, r in zip(spec.hypers, raw)]
+    return all(np.isfinite(v) for v in nat) and not any(v <= 0.0 for h, v in zip(spec.hypers, nat)
+                                                        if h.name in ("lengthscale", "outputscale", "noise"))
+
+
+def _loss_grad(spec: HyperSpec, raw, g: dict, n: int):
+    """(loss, dloss/draw) of one output: (-log p(y) - sum_priors log prior) / n from the natural-parameter gradient
+    dict ``g`` (ExactMarginalLogLikelihood's value divided by num_data [upstream])."""
+    loss = g["nll"]
+    grad = np.empty(len(spec.hypers))
+    for i, (h, r) in enumerate(zip(spec.hypers, raw)):
+        nat = h.to_natural(float(r))
+        dn = g[h.name][h.index] if h.index is not None else g[h.name]
+        if h.prior is not None:
+            loss -= h.prior.log_prob(nat)
+            dn = dn - h.prior.dlog_prob(nat)
+        grad[i] = dn * h.dnat_draw(float(r))
+    return loss / n, grad / n
+
+
 def objective(spec: HyperSpec, value_grad: Callable, n: int):
     """loss(raw), dloss/draw with value_grad(params) -> dict of -log p(y) and its natural-parameter gradient
     (engine.mll_value_grad or the oracle's mll_value_grad)."""
 
     def f(raw):
         raw = np.asarray(raw, dtype=np.float64)
-        p = spec.params_from_raw(raw)
-        # A line-search trial point outside the parameter domain (a softplus underflowing to 0, an overflow) or a
-        # Gram matrix that stays indefinite through the jitter ladder scores +inf, so L-BFGS-B backtracks (GPyTorch's
-        # NaN loss plays that role in fit_gpytorch_mll_scipy [upstream]).
-        nat = [h.to_natural(float(r)) for h, r in zip(spec.hypers, raw)]
-        if not all(np.isfinite(v) for v in nat) or any(v <= 0.0 for h, v in zip(spec.hypers, nat)
-                                                        if h.name in ("lengthscale", "outputscale", "noise")):
+        if not _feasible(spec, raw):
             return np.inf, np.zeros_like(raw)
         try:
-            g = value_grad(p)
-        except (GPXError, np.linalg.LinAlgError):
+            g = value_grad(spec.params_from_raw(raw))
+        except (GPXError, np.linalg.LinAlgError):  # indefinite through the jitter ladder: +inf, L-BFGS-B backtracks
             return np.inf, np.zeros_like(raw)
         if not np.isfinite(g["nll"]):
             return np.inf, np.zeros_like(raw)
-        loss = g["nll"]
+        return _loss_grad(spec, raw, g, n)
+
+    return f
+
+
+def objective_outputs(specs: Sequence[HyperSpec], value_grad_all: Callable, n: int):
+    """The multi-output loss over the concatenated raw vector [raw_0, raw_1, ...]: the sum of the per-output losses
+    (BoTorch's fit_gpytorch_mll on a batched model sums the batch of ExactMarginalLogLikelihood values, each with its
+    own prior terms [upstream]); value_grad_all(list of params) -> list of per-output dicts (one batched evaluation)."""
+    sizes = [len(sp.hypers) for sp in specs]
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+
+    def f(raw):
+        raw = np.asarray(raw, dtype=np.float64)
+        parts = [raw[offs[t]:offs[t + 1]] for t in range(len(specs))]
+        if not all(_feasible(sp, r) for sp, r in zip(specs, parts)):
+            return np.inf, np.zeros_like(raw)
+        try:
+            gs = value_grad_all([sp.params_from_raw(r) for sp, r in zip(specs, parts)])
+        except (GPXError, np.linalg.LinAlgError):
+            return np.inf, np.zeros_like(raw)
+        if not all(np.isfinite(g["nll"]) for g in gs):
+            return np.inf, np.zeros_like(raw)
+        loss = 0.0
         grad = np.empty_like(raw)
-        for i, (h, r) in enumerate(zip(spec.hypers, raw)):
-            nat = h.to_natural(float(r))
-            dn = g[h.name][h.index] if h.index is not None else g[h.name]
-            if h.prior is not None:
-                loss -= h.prior.log_prob(nat)
-                dn = dn - h.prior.dlog_prob(nat)
-            grad[i] = dn * h.dnat_draw(float(r))
-        return loss / n, grad / n
+        for t, (sp, r, g) in enumerate(zip(specs, parts, gs)):
+            lt, gt = _loss_grad(sp, r, g, n)
+            loss += lt
+            grad[offs[t]:offs[t + 1]] = gt
+        return loss, grad
 
     return f
 
@@ -267,3 +304,53 @@ def fit_hyperparameters(engine, X, y, kind: str = "rbf", prior_set: str = "dim_s
     loss, _ = f(res.x)
     return MLLFitResult(params=p, loss=float(loss), nll=float(final["nll"]), n_evals=int(res.nfev),
                         success=bool(res.success), message=str(res.message), raw=res.x.copy())
+
+
+@dataclass
+class MLLFitOutputsResult:
+    params: List[KernelParams]  # one per output
+    loss: float                 # final sum over outputs of (-mll_t)
+    nll: List[float]            # final -log p(y_t) per output
+    n_evals: int
+    success: bool
+    message: str
+    raw: np.ndarray = field(default_factory=lambda: np.zeros(0))
+
+
+def fit_hyperparameters_outputs(engine, X, Y, kind: str = "rbf", prior_set: str = "dim_scaled",
+                                bases: Optional[Sequence[KernelParams]] = None, fit_mean: bool = True,
+                                options: Optional[dict] = None, value_grad_all: Optional[Callable] = None,
+                                x0: Optional[Sequence[float]] = None) -> MLLFitOutputsResult:
+    """Hyperparameters of T independent outputs on one X (Y: n x T), each output its own set — the multi-output
+    SingleTaskGP's fit_gpytorch_mll (optimization/Bayesian1.py:114-115 [upstream]): ONE L-BFGS-B over the concatenated
+    raw vector on the summed loss.  Every evaluation is one batched fit of all outputs and one batched gradient
+    (GPEngine.mll_value_grad_outputs); tests inject the oracle through ``value_grad_all``."""
+    from scipy.optimize import minimize
+
+    Xn = np.asarray(X.cpu() if hasattr(X, "cpu") else X, dtype=np.float64)
+    Yn = np.asarray(Y.cpu() if hasattr(Y, "cpu") else Y, dtype=np.float64)
+    Yn = Yn.reshape(-1, 1) if Yn.ndim == 1 else Yn
+    n, d = Xn.shape
+    T = Yn.shape[1]
+    bases = list(bases) if bases is not None else [None] * T
+    if len(bases) != T:
+        raise ValueError(f"expected {T} base parameter sets, got {len(bases)}")
+    specs = [default_spec(kind, d, prior_set, bases[t], fit_mean) for t in range(T)]
+    if value_grad_all is None:
+        state = [None]
+
+        def value_grad_all(ps):
+            res, state[0] = engine.mll_value_grad_outputs(X, Y, ps, states=state[0])
+            return res
+
+    f = objective_outputs(specs, value_grad_all, n)
+    start = np.concatenate([sp.x0() for sp in specs]) if x0 is None else np.asarray(x0, dtype=np.float64)
+    bounds = [b for sp in specs for b in sp.bounds()]
+    res = minimize(f, start, jac=True, method="L-BFGS-B", bounds=bounds, options=options or {})
+    sizes = np.concatenate([[0], np.cumsum([len(sp.hypers) for sp in specs])])
+    ps = [sp.params_from_raw(res.x[sizes[t]:sizes[t + 1]]) for t, sp in enumerate(specs)]
+    final = value_grad_all(ps)
+    loss, _ = f(res.x)
+    return MLLFitOutputsResult(params=ps, loss=float(loss), nll=[float(g["nll"]) for g in final],
+                               n_evals=int(res.nfev), success=bool(res.success), message=str(res.message),
+                               raw=res.x.copy())

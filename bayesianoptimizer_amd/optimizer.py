@@ -9,10 +9,12 @@ The contract with the reference's caller is kept exactly; everything behind it i
 * persistence — the results CSV is the run's source of truth: same columns (``n,eta,sigma_y,width,height,x_01..``),
   same ``%.8f`` rows, resume by reloading it (``Bayesian7.py:268-318``); metrics go to ``validation_log.csv``.
 
-Behind it: the surrogate is an exact GP on the gpx engine (fp64, ONE factorisation shared by the 8 outputs) instead of
-the batched SVGP; its hyperparameters are fitted by exact marginal likelihood on the GPU each round (mll.py) or held
-fixed, in which case new observations are folded in by the bordered Cholesky (``ExactGP.append_observations``)
-instead of a refit.  Acquisition modes (``acquisition=``):
+Behind it: the surrogate is an exact GP on the gpx engine (fp64) instead of the batched SVGP.  Its hyperparameters are
+fitted by exact marginal likelihood on the GPU each round (mll.py) — one set PER OUTPUT, the reference's multi-output
+SingleTaskGP (optimization/Bayesian1.py:108-116; ``GPConfig.independent_outputs``), the 8 outputs fitted in one batched
+call — or held fixed and shared by the outputs (one factorisation with 8 right-hand sides, exact when the
+hyperparameters are tied), in which case new observations are folded in by the bordered Cholesky
+(``ExactGP.append_observations``) instead of a refit.  Acquisition modes (``acquisition=``):
 
 * ``"variance"`` (default, Bayesian7's pool scan ``:646-688``): Latin-hypercube pool -> summed posterior variance on
   the device -> top-K on the device (``gpx_topk_f64``, deterministic ties) -> farthest-point sampling on the device
@@ -65,6 +67,9 @@ class GPConfig:
     # exact marginal likelihood each round (fit_gpytorch_mll, Bayesian.py:92-93; the driven variant trains by ELBO,
     # Bayesian7.py:451-538); False keeps the values above
     fit_hyperparameters: bool = True
+    # with fit_hyperparameters: one hyperparameter set per output (lengthscales, outputscale, noise, constant mean), as
+    # BoTorch's multi-output SingleTaskGP fits them (Bayesian1.py:108-116 [upstream]); False: one set shared by all
+    independent_outputs: bool = True
     prior_set: str = "none"               # "none" (ScaleKernel(Linear + Matern) of Bayesian6/7) | "dim_scaled" | "gamma"
     mll_options: Optional[dict] = None    # scipy L-BFGS-B options
     # with fixed hyperparameters: freeze the input standardisation at the first fit and fold each round's new rows in
@@ -284,7 +289,8 @@ class BayesianOptimizer:
         self._check_device_budget(n, n)
         self.x_tf = LogInputStandardizer(self._bounds_t()).fit(self.train_X)
         self.gp_model = ExactGP(self.x_tf(self.train_X), Ys, self._kernel_params(), engine=self.engine,
-                                jitter_schedule=reference_jitter_schedule(cfg.jitter_val))
+                                jitter_schedule=reference_jitter_schedule(cfg.jitter_val),
+                                independent_outputs=cfg.fit_hyperparameters and cfg.independent_outputs)
         if cfg.fit_hyperparameters:
             self.gp_model.fit_hyperparameters(cfg.prior_set, options=cfg.mll_options)
         else:
@@ -349,7 +355,8 @@ class BayesianOptimizer:
             m = int(self.svgp_threshold)
             sub = np.sort(self._subsample_rng.choice(n, size=m, replace=False))
             sub_t = torch.as_tensor(sub, device=Xs.device)
-            sub_gp = ExactGP(Xs[sub_t], Ys[sub_t], params, engine=self.engine, jitter_schedule=jit)
+            sub_gp = ExactGP(Xs[sub_t], Ys[sub_t], params, engine=self.engine, jitter_schedule=jit,
+                             independent_outputs=cfg.independent_outputs or not isinstance(params, KernelParams))
             sub_gp.fit_hyperparameters(cfg.prior_set, options=cfg.mll_options)
             params = sub_gp.params
             del sub_gp
@@ -443,9 +450,12 @@ class BayesianOptimizer:
         cfg = self.config
         gp = self.gp_model
         pool = self._tensor(self._latin_hypercube(cfg.candidates_pool_size))
-        _, _, score = gp.engine.acquire(gp.state, self.x_tf(pool), "variance", return_scores=True)
-        # every output's variance is var_std * s_t^2 with s_t = 1 in the log-standardised space: the summed score
-        # ranks like the shared variance
+        if gp.independent:  # sum over the outputs of their own posterior variances, in one device sweep
+            _, _, score = gp.engine.acquire_multi(gp.states, self.x_tf(pool), "variance", return_scores=True)
+        else:
+            # every output's variance is the shared var_std (s_t = 1 in the log-standardised space): the summed score
+            # ranks like the shared variance
+            _, _, score = gp.engine.acquire(gp.state, self.x_tf(pool), "variance", return_scores=True)
         k_big = min(max(5000, 20 * k), cfg.K_BIG_CAP, pool.shape[0])
         _, order = self.engine.topk(score, k_big)
         shortlist = pool[order.to(pool.device)]
@@ -454,26 +464,15 @@ class BayesianOptimizer:
         start = int(self._rng.integers(0, k_big))
         return shortlist[self.engine.fps(shortlist, k, start).to(pool.device)]
 
-    def _objective_sweep_args(self, w: torch.Tensor) -> dict:
-        """(alpha, y_mean, y_scale) that make the engine's sweep score the objective sum_t w_t f_t (f_t the modelled
-        outputs, sharing the covariance and the constant mean c): mean c sum(w) + k*^T sum_t w_t alpha_t, variance
-        |w|^2 var.  The engine computes y_mean + y_scale (c + k*^T alpha'), y_scale^2 var, hence
-        y_scale = |w|, alpha' = sum_t w_t alpha_t / |w|, y_mean = c (sum(w) - |w|)."""
-        st = self.gp_model.state
-        w = w.to(device=st.alpha.device, dtype=torch.float64)
-        s = float(torch.linalg.vector_norm(w))
-        if s == 0.0:
-            raise ValueError("objective weights are all zero")
-        c = float(st.params.const_mean)
-        alpha = (st.alpha[:, : w.numel()] @ w) / s
-        return {"alpha": alpha.contiguous(), "y_mean": c * (float(w.sum()) - s), "y_scale": s}
-
     def _analytic_sweep(self, k: int) -> torch.Tensor:
+        """Sobol grid scored on the objective sum_t w_t f_t of the modelled outputs (ExactGP.sweep_objective: the
+        combined alpha of one shared factorisation, or the multi-output sweep over independent outputs), best k by
+        gpx_topk_f64."""
         gp = self.gp_model
         grid = self._tensor(self._sobol_grid(self.config.raw_samples))
         w = self._acq_weights()
-        _, _, score = gp.engine.acquire(gp.state, self.x_tf(grid), self.acquisition, best_f=self._incumbent(w),
-                                        beta=self.config.beta, return_scores=True, **self._objective_sweep_args(w))
+        _, _, score = gp.sweep_objective(self.x_tf(grid), self.acquisition, w.tolist(), best_f=self._incumbent(w),
+                                         beta=self.config.beta, return_scores=True)
         _, order = self.engine.topk(score, min(k, grid.shape[0]))
         return grid[order.to(grid.device)]
 
@@ -545,8 +544,10 @@ class BayesianOptimizer:
         ok = sum(self._observe(x) for x in batch)
         if ok:
             try:  # the model is recomputable from the CSV; this snapshot is a convenience
-                torch.save({"X": self.train_X.cpu(), "Y": self.train_Y_raw.cpu(),
-                            "kernel": dict(self.gp_model.params.__dict__)}, self.model_save_path)
+                ps = self.gp_model.params
+                kernel = [dict(p.__dict__) for p in ps] if isinstance(ps, list) else dict(ps.__dict__)
+                torch.save({"X": self.train_X.cpu(), "Y": self.train_Y_raw.cpu(), "kernel": kernel},
+                           self.model_save_path)
             except Exception:
                 pass
         return ok

@@ -134,10 +134,12 @@ size_t gpx_acq_params_size(void);
  * variable GPX_OPTIONS once ("name=value,name=value", names as below in lower case without the prefix, e.g.
  * "sweep_fused=0,potrf_mode=1"; an unknown name is reported on stderr and ignored); nothing else in the library reads
  * the environment.  The numbers are stable ABI: a removed option keeps its slot as GPX_OPT_RESERVED_n, which
- * gpx_set_option / gpx_get_option reject with GPX_INVALID_ARG.  None of the options changes a result bit: the Cholesky
- * schedules are arithmetic-invariant (any schedule that folds the forward substitution - every default, and every
- * potrf_mode 1 or potrf_lazy 1 setting - gives the same L, z and alpha; potrf_mode 0 with potrf_lazy > 1 runs the
- * forward substitution as a separate solve, so only alpha's rounding differs there).
+ * gpx_set_option / gpx_get_option reject with GPX_INVALID_ARG.  The Cholesky schedule options (potrf_*) and gram_split
+ * change no result bit: the schedules are arithmetic-invariant (any schedule that folds the forward substitution - every
+ * default, and every potrf_mode 1 or potrf_lazy 1 setting - gives the same L, z and alpha; potrf_mode 0 with
+ * potrf_lazy > 1 runs the forward substitution as a separate solve, so only alpha's rounding differs there).
+ * sweep_fused = 0 takes the K* + trmm path at padded n <= 256, which sums in a different order: its results agree with
+ * the fused path to the parity tolerance, not bit for bit.
  *  GPX_OPT_RESERVED_0      (was GPX_OPT_POTRF_SCHEDULE, removed in 0.4)
  *  GPX_OPT_SPIN_LIMIT      polls before an in-launch hand-off (the triangular solve's) gives up and
  *                          reports GPX_INFO_TIMEOUT (default 4194304; 0 = give up at the first unmet poll: tests)
@@ -229,8 +231,10 @@ gpx_status gpx_fit_factor_f64(gpx_handle h, const gpx_kernel_params* p, int64_t 
 
 /* Batched posterior updates: `batch` independent problems of the same n, d and kernel parameters (restarts /
  * seeds: BASELINE configs[3], the per-batch `info` of the SURVEY §8b proposal) in the SAME launches, the problem
- * index being one more grid dimension.  Every array of problem b starts at base + b * stride_* (element strides,
- * >= one problem); info: device int32[batch], each 0 or that problem's failing pivot + 1.  Results are identical bit for
+ * index being one more grid dimension.  Every array of problem b starts at base + b * stride_* (element strides;
+ * outputs K / Dinv / W / alpha >= one problem; the read-only X and Y any stride >= 0: X stride 0 = one X shared by
+ * every problem, Y stride 1 with ldy = batch = column b of an n x batch target matrix); info: device int32[batch],
+ * each 0 or that problem's failing pivot + 1.  Results are identical bit for
  * bit to `batch` calls of gpx_fit_f64 with the default options, although the batch may take a different Cholesky
  * schedule (every schedule computes each factor entry by the same MFMA chain, gpx_potrf.hip trailing_tile_at), so a
  * problem's result does not depend on how many problems share its GPU.  The Cholesky is a latency-bound chain of nblk dependent launches, so a batch of B
@@ -248,6 +252,25 @@ gpx_status gpx_fit_factor_batched_f64(gpx_handle h, const gpx_kernel_params* p, 
                                       int64_t stride_y, int64_t nrhs, double* K, int64_t ldk, int64_t stride_k,
                                       double* Dinv, int64_t stride_dinv, double* alpha, int64_t stride_alpha,
                                       int32_t* info, void* ws, size_t ws_bytes);
+
+/* The same with ONE PARAMETER SET PER PROBLEM: p points to `batch` parameter structs of the same d (any kind, lengthscales,
+ * outputscale, linear variances, noise, jitter and constant mean).  This is the reference's multi-output SingleTaskGP
+ * (optimization/Bayesian1.py:108-116: SingleTaskGP(X, Y[n, 8], Standardize(m=8)), a batch of 8 independent GPs on one X,
+ * each with its own lengthscales, outputscale, noise and ConstantMean [upstream]; optimization/Bayesian6.py:474-478
+ * shares the covariance module, but its likelihood noise and mean are still per output): X stride 0, Y stride 1 with
+ * ldy = batch and nrhs = 1.  The covariance of each problem is built with its own parameters (one Gram launch per
+ * problem when they differ), the Cholesky and the solves run once over all problems; a problem's result is bit for bit
+ * the single fit with its parameters.  Workspace sizes as for the shared-parameter entry points. */
+gpx_status gpx_fit_batched_params_f64(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n,
+                                      const double* X, int64_t ldx, int64_t stride_x, const double* Y, int64_t ldy,
+                                      int64_t stride_y, int64_t nrhs, double* K, int64_t ldk, int64_t stride_k,
+                                      double* Dinv, int64_t stride_dinv, double* W, int64_t ldw, int64_t stride_w,
+                                      double* alpha, int64_t stride_alpha, int32_t* info, void* ws, size_t ws_bytes);
+gpx_status gpx_fit_factor_batched_params_f64(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n,
+                                             const double* X, int64_t ldx, int64_t stride_x, const double* Y,
+                                             int64_t ldy, int64_t stride_y, int64_t nrhs, double* K, int64_t ldk,
+                                             int64_t stride_k, double* Dinv, int64_t stride_dinv, double* alpha,
+                                             int64_t stride_alpha, int32_t* info, void* ws, size_t ws_bytes);
 
 /* Incremental posterior update: rows n_old .. n_new-1 of X / Y appended to a GP whose L, Dinv and W
  * hold a successful fit (gpx_fit_f64 or an earlier append) of the first n_old rows with the SAME kernel parameters.
@@ -286,6 +309,26 @@ gpx_status gpx_acquire_argmax_f64(gpx_handle h, const gpx_kernel_params* p, int6
                                   const double* Xs, int64_t m, int64_t ldxs, const gpx_acq_params* a,
                                   int64_t index_offset, double* best_val, int64_t* best_idx,
                                   double* scores_out, void* ws, size_t ws_bytes);
+
+/* Candidate sweep of a LINEAR OBJECTIVE over T independent GPs on the same training inputs X (the outputs of the batched
+ * fits above, or of separate fits / appends of the same n): f = sum_t w_t (y_mean[t] + y_scale[t] g_t) with g_t the
+ * posterior of output t: its own p[t], W_host[t] (device pointer to its W = L^{-T}, leading dim ldw_host[t]) and
+ * alpha_host[t] (device pointer to its padded_n alpha column); W_host / ldw_host / alpha_host are host arrays of T.  So mean = sum_t w_t (y_mean[t] +
+ * y_scale[t] mu_t) and, the outputs being independent, variance = sum_t w_t^2 y_scale[t]^2 var_t (each var_t floored at
+ * 1e-10 in its standardised space, the sum at 1e-12: GPyTorch's / BoTorch's floors [upstream]).  Scored with a's kind /
+ * best_f / beta (a->y_mean, a->y_scale are not used: the per-output y_mean_host / y_scale_host are, NULL = 0 / 1) and
+ * reduced like gpx_acquire_argmax_f64.  VARIANCE with w_t = 1 is the variance-sum pool-scan score of
+ * optimization/Bayesian7.py:671 over independent outputs; EI / LogEI / UCB with weights the scalarised objective of a
+ * multi-output model (optimization/Bayesian1.py:119-140's mean-of-8 objective, analytic form).  T = 1, w = 1 gives
+ * gpx_acquire_argmax_f64's scores bit for bit. */
+gpx_status gpx_sweep_multi_workspace_size(int64_t n, int64_t m, size_t* bytes);
+gpx_status gpx_acquire_argmax_multi_f64(gpx_handle h, const gpx_kernel_params* p, int64_t T, int64_t n, const double* X,
+                                        int64_t ldx, const double* const* W_host, const int64_t* ldw_host,
+                                        const double* const* alpha_host, const double* weights_host,
+                                        const double* y_mean_host, const double* y_scale_host, const double* Xs,
+                                        int64_t m, int64_t ldxs, const gpx_acq_params* a, int64_t index_offset,
+                                        double* best_val, int64_t* best_idx, double* scores_out, void* ws,
+                                        size_t ws_bytes);
 
 /* Deterministic (value, index) reduction of `count` device records: max value, then lowest index; NaN
  * never wins.  Used after the cross-GPU all-gather of per-rank records. */
@@ -337,10 +380,21 @@ gpx_status gpx_allreduce_argmax(gpx_handle h, gpx_comm c, double* best_val, int6
  * (fixed reduction order).  Replaces ExactMarginalLogLikelihood(...).backward() inside fit_gpytorch_mll
  * [upstream] (optimization/Bayesian.py:92-93, optimization/Bayesian1.py:114-115, optimization/Bayesian6.py:480-488). */
 gpx_status gpx_mll_workspace_size(int64_t n, size_t* bytes);
+/* (the batched form is below) */
 gpx_status gpx_mll_grad_f64(gpx_handle h, const gpx_kernel_params* p, int64_t n, const double* X, int64_t ldx,
                             const double* Y, int64_t ldy, int64_t nrhs, const double* L, int64_t ldl,
                             const double* W, int64_t ldw, const double* alpha, double* out, void* ws,
                             size_t ws_bytes);
+
+/* The same for `batch` independent problems with one parameter set each (the fits of gpx_fit_batched_params_f64):
+ * problem b's X, Y, L, W, alpha at base + b * stride_* (X / Y strides >= 0, as in the batched fit), its output vector at
+ * out + b * GPX_MLL_NOUT.  The reference's multi-output fit_gpytorch_mll minimises the SUM of the per-output losses
+ * (optimization/Bayesian1.py:114-115 [upstream]); the host side (mll.py) sums them.  Workspace: gpx_mll_workspace_size. */
+gpx_status gpx_mll_grad_batched_f64(gpx_handle h, const gpx_kernel_params* p, int64_t batch, int64_t n, const double* X,
+                                    int64_t ldx, int64_t stride_x, const double* Y, int64_t ldy, int64_t stride_y,
+                                    int64_t nrhs, const double* L, int64_t ldl, int64_t stride_l, const double* W,
+                                    int64_t ldw, int64_t stride_w, const double* alpha, int64_t stride_alpha,
+                                    double* out, void* ws, size_t ws_bytes);
 
 /* ---- SVGP predictive + pool-scan selection: the driven variant ---------------- */
 /* optimization/Bayesian7.py's BatchSVGP (ntask outputs, each with its own ScaleKernel(Linear + Matérn-5/2)

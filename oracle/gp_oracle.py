@@ -370,6 +370,34 @@ def posterior(state: GPState, Xs: np.ndarray, y_mean: float = 0.0, y_scale: floa
     return mu, var
 
 
+def fit_outputs(X: np.ndarray, Y: np.ndarray, params: Sequence[KernelParams]):
+    """T independent GPs on one X (Y: n x T, one KernelParams per output): the reference's multi-output SingleTaskGP,
+    optimization/Bayesian1.py:108-116 (a batch of independent GPs, each with its own hyperparameters [upstream])."""
+    Y = np.asarray(Y, dtype=np.float64)
+    return [fit(X, Y[:, t], params[t]) for t in range(Y.shape[1])]
+
+
+def objective_posterior(states: Sequence[GPState], Xs: np.ndarray, weights, y_mean=None, y_scale=None):
+    """Posterior of f = sum_t w_t (y_mean_t + y_scale_t g_t) over independent outputs g_t: mean sum_t w_t (y_mean_t +
+    y_scale_t mu_t), variance sum_t w_t^2 y_scale_t^2 var_t (GPyTorch's 1e-10 floor per output, BoTorch's 1e-12 on the
+    sum [upstream]) — BoTorch's ScalarizedPosteriorTransform of a batched multi-output posterior, analytic form."""
+    T = len(states)
+    ym = np.zeros(T) if y_mean is None else np.asarray(y_mean, dtype=np.float64)
+    ys = np.ones(T) if y_scale is None else np.asarray(y_scale, dtype=np.float64)
+    w = np.asarray(weights, dtype=np.float64)
+    mu = np.zeros(Xs.shape[0])
+    var = np.zeros(Xs.shape[0])
+    for t, st in enumerate(states):
+        p = st.params
+        Ks = kernel_matrix(st.X, Xs, p)
+        m_t = (p.const_mean + Ks.T @ st.alpha).reshape(-1)  # alpha: (n,) or one column (n, 1)
+        V = sla.solve_triangular(st.L, Ks, lower=True, check_finite=False)
+        v_t = np.maximum(kernel_diag(Xs, p) - np.einsum("ij,ij->j", V, V), GPYTORCH_MIN_VAR_F64)
+        mu += w[t] * (ym[t] + ys[t] * m_t)
+        var += w[t] * w[t] * (ys[t] * ys[t] * v_t)
+    return mu, np.maximum(var, BOTORCH_MIN_VAR)
+
+
 # ---------------------------------------------------------------------------------------------
 # a7: analytic acquisition (BoTorch analytic forms, restated)
 # ---------------------------------------------------------------------------------------------

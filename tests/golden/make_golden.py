@@ -108,6 +108,8 @@ RESULTS_FILES = {  # tag -> file under results/ 
     "r4235": "optimization_results1012.csv",
     "r5000": "optimization_results2.csv",
     "r7740": "optimization_results1009.csv",
+    "r2905": "optimization_results002.csv",     # legacy disp_1..8 header: columns are taken by position
+    "r173": "optimization_results100917.csv",   # small n: below the npad = 256 fused-sweep boundary
 }
 
 

@@ -31,6 +31,7 @@ class OState:
     n: int
     nrhs: int
     params: object
+    info: int = 0  # 0 or failing pivot + 1 (fit_outputs with check=False)
 
 
 class OracleEngine:
@@ -51,6 +52,44 @@ class OracleEngine:
         except O.NotPDError as e:
             raise NotPositiveDefiniteError(e.pivot)
         return OState(st, torch.tensor(st.alpha.reshape(X.shape[0], -1)), X.shape[0], Y.shape[1], params)
+
+    def fit_outputs(self, X, Y, params, check=True, out=None, inverse=False):
+        """T independent outputs on one X, one parameter set each (GPEngine.fit_outputs)."""
+        self.calls["fit_outputs"] = self.calls.get("fit_outputs", 0) + 1
+        X = torch.as_tensor(X, dtype=torch.float64).cpu().numpy()
+        Y = torch.as_tensor(Y, dtype=torch.float64).cpu().numpy()
+        states = []
+        for t, p in enumerate(params):
+            try:
+                st = O.fit(X, Y[:, t], to_oracle_params(p, X.shape[1]))
+                states.append(OState(st, torch.tensor(st.alpha.reshape(-1, 1)), X.shape[0], 1, p))
+            except O.NotPDError as e:
+                if check:
+                    raise NotPositiveDefiniteError(e.pivot)
+                dummy = O.GPState(X=X, L=np.eye(X.shape[0]), alpha=np.zeros(X.shape[0]), params=None)
+                states.append(OState(dummy, torch.zeros((X.shape[0], 1)), X.shape[0], 1, p, info=e.pivot + 1))
+        return states
+
+    @staticmethod
+    def batch_info(states):
+        return np.array([s.info for s in states], dtype=np.int64)
+
+    def acquire_multi(self, states, Xs, kind="logei", best_f=0.0, beta=4.0, weights=None, y_mean=None, y_scale=None,
+                      index_offset=0, return_scores=False):
+        self.calls["acquire_multi"] = self.calls.get("acquire_multi", 0) + 1
+        Xs = torch.as_tensor(Xs, dtype=torch.float64).cpu().numpy()
+        T = len(states)
+        w = np.ones(T) if weights is None else np.asarray(weights, dtype=np.float64)
+        mu, var = O.objective_posterior([s.st for s in states], Xs, w, y_mean, y_scale)
+        scores = O.acquisition(mu, var, ACQS[kind] if isinstance(kind, str) else int(kind), best_f, beta)
+        v, i = O.argmax_lowest(scores)
+        out = (torch.tensor([v], dtype=torch.float64), torch.tensor([i + index_offset], dtype=torch.int64))
+        return out + (torch.tensor(scores),) if return_scores else out
+
+    def mll_value_grad_outputs(self, X, Y, params, jitters=(0.0, 1e-8, 1e-7, 1e-6), states=None):
+        self.calls["mll"] = self.calls.get("mll", 0) + 1
+        Y = torch.as_tensor(Y, dtype=torch.float64)
+        return [self.mll_value_grad(X, Y[:, t], p, jitters)[0] for t, p in enumerate(params)], None
 
     def mll_value_grad(self, X, Y, params, jitters=(0.0, 1e-8, 1e-7, 1e-6), state=None):
         self.calls["mll"] = self.calls.get("mll", 0) + 1

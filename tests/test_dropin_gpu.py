@@ -64,7 +64,9 @@ def test_dropin_crosses_svgp_threshold_on_gpu(tmp_path, engine):
     gp = opt.gp_model
     assert opt.train_X.shape[0] == 3050
     assert opt._large_n_base == 3010          # the first round above the threshold rebuilt the factor
-    assert gp.state.n == 3050                 # the rows since were folded in by the bordered update
+    assert gp.independent                      # hyperparameters per output (the multi-output SingleTaskGP)
+    assert all(st.n == 3050 for st in gp.states)  # the rows since were folded in by the bordered update, per output
+    assert len({tuple(p.lengthscales(5)) for p in gp.params}) > 1
     ref = ExactGP(gp.train_X, opt.y_tf(opt.train_Y_raw), gp.params, engine=engine).fit()
     Xq = opt.x_tf(torch.tensor(O.sobol_candidates(512, 5, 3), device=engine.device))
     a, b = gp.posterior(Xq), ref.posterior(Xq)
@@ -72,7 +74,8 @@ def test_dropin_crosses_svgp_threshold_on_gpu(tmp_path, engine):
     assert (a.mean - b.mean).abs().max() <= 1e-9 * scale
     # the parity scale of a variance is the prior variance k(x, x) >= outputscale, not the posterior
     # variance, which at 3050 points is ~1e-6 (bordered update vs refit measured 4.6e-12 absolute)
-    assert (a.variance - b.variance).abs().max() <= 1e-9 * gp.params.outputscale
+    os_min = min(p.outputscale for p in gp.params)
+    assert (a.variance - b.variance).abs().max() <= 1e-9 * os_min
 
 
 def test_dropin_survives_timed_out_handoffs(tmp_path, engine):

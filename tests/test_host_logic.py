@@ -181,8 +181,7 @@ def test_dropin_analytic_sweep_scores_the_reported_objective(tmp_path, mode, acq
     Xq = torch.tensor(O.sobol_candidates(64, 5, 9))
     Xt = opt.x_tf(Xq)
     best_f = opt._incumbent(w)
-    _, _, got = eng.acquire(gp.state, Xt, acq, best_f=best_f, beta=4.0, return_scores=True,
-                            **opt._objective_sweep_args(w))
+    _, _, got = gp.sweep_objective(Xt, acq, w.tolist(), best_f=best_f, beta=4.0, return_scores=True)
     # reference: per-output posteriors (each with the constant mean), combined
     st = gp.state.st
     wn = w.numpy()

@@ -167,7 +167,8 @@ def test_reference_results_fixtures():
     """The full-size reference data of tests/test_gpu_realdata.py: row counts of the five results files (one corrupt row
     of optimization_results2.csv dropped), the 1550 duplicate X rows of optimization_results1009.csv, the validation
     rows, and the oracle's jitter choice on the duplicate file's head (noise-free: fails at jitter 0, taken at 1e-4)."""
-    rows = {"r3000": (3000, 2), "r3901": (3901, 0), "r4235": (4235, 7), "r5000": (5000, 0), "r7740": (7740, 1550)}
+    rows = {"r3000": (3000, 2), "r3901": (3901, 0), "r4235": (4235, 7), "r5000": (5000, 0), "r7740": (7740, 1550),
+            "r2905": (2905, 0), "r173": (173, 2)}
     for tag, (n, dup) in rows.items():
         z = np.load(os.path.join(GOLDEN, f"results_{tag}.npz"))
         assert z["X"].shape == (n, 5) and z["Y"].shape == (n, 8) and int(z["duplicate_rows"]) == dup, tag
