@@ -204,8 +204,14 @@ __device__ __forceinline__ void chol16_store(const Blk16& b, double* sA, double*
 }
 
 // L_cc[r][c] (c <= r) of a factored 64x64 diagonal tile whose 16x16 diagonal blocks hold U (chol16_store) and whose
-// blocks below them hold L (the T step): the diagonal blocks give L[r][c] = U[c][r] / sqrt(U[c][c]) (the pivot_rsq of
-// the chain, recomputed from the same pivot: the same bits), isq: 64 doubles of scratch filled by l64_isq.
+// blocks below them hold L (the T step): the diagonal blocks give L[r][c] = U[c][r] * isq[c], with isq[c] = pivot_rsq of
+// the pivot (recomputed from the same pivot, so the same isq bits as the chain's).  The stored L_cc is NOT bit-equal to a
+// capture of the column operations: U's rows come from the unscaled rank-1 updates (round(a_r * rinv) * a_c is not
+// bitwise symmetric with round(a_c * rinv) * a_r), while D = b.x, the T step's L_ic = A_ic D^T and the folded z use the
+// column operations — the two differ at rounding level (the Dinv that potrs later forms from L_cc differs from the
+// panel's D in the last bits).  Harmless for the results (tests/test_gpu_parity.py checks the factor's backward error
+// ||L L^T - K|| / ||K|| at n = 4096 and 16384), and schedule-invariant: every schedule stores L_cc the same way.
+// isq: 64 doubles of scratch filled by l64_isq.
 __device__ __forceinline__ void l64_isq(const double* sA, double* isq) {
   const int t = threadIdx.x;
   if (t < 64) isq[t] = pivot_rsq(sA[t * LD64 + t]);

@@ -576,6 +576,23 @@ def test_fit_batched_reports_not_pd_per_problem(engine):
         engine.fit_batched(t(Xs), t(np.zeros((B, n))), kp)
 
 
+@pytest.mark.parametrize("n,kind", [(4096, "rbf"), (16384, "matern52")])
+def test_factor_backward_error(engine, n, kind):
+    """||L L^T - K||_F / ||K||_F of the whole factor on the device (L_cc is built from U's rows while D and the
+    T step use the column operations, so the stored L_cc and the panel's D differ at rounding level): the factor the
+    default update leaves must stay backward stable, at the configs[1] and configs[2] sizes."""
+    d = 8
+    X, y = O.synthetic_problem(n, d, 3)
+    kp, _ = pair(kind, d, noise=1e-4)
+    K = engine.gram(t(X), kp)[:n, :n]
+    K = torch.tril(K) + torch.tril(K, -1).T
+    st = engine.fit(t(X), t(y), kp)
+    L = torch.tril(st.L[:n, :n])
+    err = float(torch.linalg.matrix_norm(L @ L.T - K) / torch.linalg.matrix_norm(K))
+    print(f"n={n} {kind}: backward error ||L L^T - K||_F / ||K||_F = {err:.2e}")
+    assert err <= 1e-13, err
+
+
 @pytest.mark.parametrize("n,kind", [(8192, "rbf"), (16384, "matern52"), (32768, "rbf")])
 def test_large_fit_inverse_and_factor_rows(engine, n, kind):
     # sizes whose TRTRI uses the 128x128-tile levels and whose Cholesky uses the lazy trailing flush

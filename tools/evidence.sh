@@ -1,7 +1,9 @@
-# Round 5 evidence set, ONE call, one box, one tree (profiles/README.md indexes the outputs):
+# The round's evidence set, ONE call, one box, one tree (profiles/README.md indexes the outputs; tools/copy_evidence.sh
+# ROUND copies them into profiles/ under the round's names):
 #  1. rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over the sweep -> trmm HBM traffic (bench.py roofline.traffic);
 #  2. SQ pass over the sweep product (MFMA busy per SIMD, wave-cycle split) and the Cholesky's MFMA-busy per launch;
-#  3. per-launch kernel trace of the n = 4096 update;
+#  3. per-launch kernel trace of the n = 4096 update, and the per-phase timeline of its launches (tools/potrf_steps_probe,
+#     built in-tree beforehand: launch gap, pre-update, the four 16-pivot blocks, factor tail, store);
 #  4. the -m gpu suite, smoke, bench (N=1), bench --problems-per-gpu 4;
 #  5. rocprofv3 --kernel-trace --stats of the bench.
 # A failing test (pytest rc 1) does not stop the measurements; a crash, abort or time limit does.
@@ -14,7 +16,8 @@ timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetc
 timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -- python3 $R/tools/sweep_only.py --m 131072 --reps 2 > $O/pmc_write.log 2>&1 &&
 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_sq -- python3 $R/tools/sweep_only.py --m 131072 --reps 2 > $O/pmc_sq.log 2>&1 &&
 timeout -s KILL 90 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE --output-format csv -d $O/pmc_potrf -- python3 $R/tools/fit_only.py --reps 3 > $O/pmc_potrf.log 2>&1 &&
-timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o fit -- python3 $R/tools/fit_only.py --n 4096 --reps 3 > $O/trace.log 2>&1 || exit $?
+timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $O/trace -o fit -- python3 $R/tools/fit_only.py --n 4096 --reps 3 > $O/trace.log 2>&1 &&
+timeout -k 10 120 $R/tools/potrf_steps_probe 4096 0 1 > $O/potrf_steps_4096.log 2>&1 || exit $?
 cd $R
 python3 tools/pmc_traffic.py trmm_sumsq $O/pmc_fetch $O/pmc_write $O/trmm_pmc_traffic.json > $O/pmc_traffic.log 2>&1 &&
 cp $O/trmm_pmc_traffic.json profiles/trmm_pmc_traffic.json &&
