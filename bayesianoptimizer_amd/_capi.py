@@ -29,7 +29,8 @@ STATUS_NAMES = {0: "OK", 1: "NOT_PD", 2: "INVALID_ARG", 3: "HIP_ERROR", 4: "RCCL
 GPX_INFO_TIMEOUT = -(2 ** 31)  # device info word of a factorisation / solve whose in-launch hand-off timed out
 
 # per-handle options (include/gpx.h GPX_OPT_*; slot 0 is GPX_OPT_RESERVED_0, the removed potrf_schedule)
-OPTIONS = {"spin_limit": 1, "sweep_fused": 2, "gram_split": 3, "potrf_lazy": 4, "potrf_mode": 5, "potrf_switch": 6}
+OPTIONS = {"spin_limit": 1, "sweep_fused": 2, "gram_split": 3, "potrf_lazy": 4, "potrf_mode": 5, "potrf_switch": 6,
+           "potrf_split": 7}
 GPX_OPT_RESERVED = (0,)
 GPX_OPT_COUNT = len(OPTIONS) + len(GPX_OPT_RESERVED)
 

@@ -200,6 +200,10 @@ static gpx_status set_option(Context* c, int32_t option, int64_t v) {
       if (v < -1 || v > 16384) return fail(c, GPX_INVALID_ARG, "potrf_switch must be in [-1, 16384]");
       c->potrf_switch = (int)v;
       return GPX_OK;
+    case GPX_OPT_POTRF_SPLIT:
+      if (v != -1 && v != 1 && v != 3) return fail(c, GPX_INVALID_ARG, "potrf_split must be -1, 1 or 3");
+      c->potrf_split = (int)v;
+      return GPX_OK;
     default:
       return fail(c, GPX_INVALID_ARG, "unknown option " + std::to_string(option));
   }
@@ -208,7 +212,7 @@ static gpx_status set_option(Context* c, int32_t option, int64_t v) {
 static int option_by_name(const std::string& name) {
   // index = GPX_OPT_* number; slot 0 is reserved (the removed potrf_schedule) and has no name
   static const char* names[GPX_OPT_COUNT] = {"", "spin_limit", "sweep_fused", "gram_split", "potrf_lazy", "potrf_mode",
-                                               "potrf_switch"};
+                                               "potrf_switch", "potrf_split"};
   for (int i = 1; i < GPX_OPT_COUNT; ++i)
     if (name == names[i]) return i;
   return -1;
@@ -258,6 +262,7 @@ gpx_status gpx_get_option(gpx_handle h, int32_t option, int64_t* value_host) {
     case GPX_OPT_POTRF_LAZY: *value_host = c->potrf_lazy; return GPX_OK;
     case GPX_OPT_POTRF_MODE: *value_host = c->potrf_mode; return GPX_OK;
     case GPX_OPT_POTRF_SWITCH: *value_host = c->potrf_switch; return GPX_OK;
+    case GPX_OPT_POTRF_SPLIT: *value_host = c->potrf_split; return GPX_OK;
     default: return fail(c, GPX_INVALID_ARG, "unknown option " + std::to_string(option));
   }
 }

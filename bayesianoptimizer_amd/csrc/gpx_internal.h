@@ -39,6 +39,7 @@ struct Context {
   int potrf_lazy = 0;      // multi-launch flush interval, 0 by size
   int potrf_mode = -1;     // multi-launch panel mode, -1 by size
   int potrf_switch = -1;   // launch at which a single fit switches schedule (gpx_potrf.hip potrf_switch), -1 by size
+  int potrf_split = -1;    // panel split policy (gpx_potrf.hip step_plan): -1 fits the slots, 1 never, 3 one per CU
 };
 
 // Scoped device switch of one C ABI call: makes the handle's device current and restores the caller's current device

@@ -757,7 +757,10 @@ struct StepPlan {
 
 // slots > 0: the co-resident workgroup slots a problem may fill (two per CU, shared by a batch); the panel row blocks are
 // split in 2 (StepPlan::split) when the panels apply exactly one column and the split launch still fits the slots.
-inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush, int xmap = 0, int slots = 0) {
+// split_policy (GPX_OPT_POTRF_SPLIT): -1 split where the launch fits the slots, 1 never, 3 only where it fits one
+// workgroup per CU (slots / 2), so that panel workgroups do not share a CU with lookahead / trailing ones
+inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush, int xmap = 0, int slots = 0,
+                          int split_policy = -1) {
   StepPlan s;
   s.npanel = nblk - c;
   s.split = 1;
@@ -779,11 +782,12 @@ inline StepPlan step_plan(int c, int nblk, int mode, int last_flush, bool flush,
   s.ntrail = M * (M + 1) / 2;
   s.xmap = xmap;
   const bool eager = mode == 1 || c == 0 || c - last_flush == 1;
-  if (slots > 0 && eager && s.npanel > 1) {
+  if (slots > 0 && eager && s.npanel > 1 && split_policy != 1) {
+    const int room = split_policy == 3 ? slots / 2 : slots;
     for (int sp = 2; sp >= 2; sp >>= 1) {  // split 4 measured slower at n = 4096 (potrf 1.48 vs 1.46 ms), equal below
       const int np = 1 + sp * (s.npanel - 1);
       const int tb = xmap ? (np + s.nlook + 7) & ~7 : np + s.nlook;
-      if (tb + s.ntrail <= slots) {
+      if (tb + s.ntrail <= room) {
         s.split = sp;
         s.npanel = np;
         break;
@@ -974,7 +978,7 @@ static void for_each_step(const Context* ctx, int nblk, int batch, int mode, int
     // 5.673 -> 5.629 ms, B = 4 x n = 4096 3.169 -> 3.163 (profiles/r05_flush_order_384_ab.log).  The n = 4096 K = 256
     // flush (one round of 465 tiles) keeps the chunks: 87.5 vs 106 us row-major (profiles/r05_potrf_launches_4096.log)
     const int xmap = (flush && c - last >= 6) ? 0 : 1;
-    f(c, step_plan(c, nblk, early ? 1 : (sw > 0 ? 0 : mode), last, flush, xmap, slots));
+    f(c, step_plan(c, nblk, early ? 1 : (sw > 0 ? 0 : mode), last, flush, xmap, slots, ctx->potrf_split));
     if (flush) last = c;
   }
 }

@@ -149,7 +149,9 @@ size_t gpx_acq_params_size(void);
  *  GPX_OPT_POTRF_MODE      multi-launch schedule: -1 by size and batch (default), 0 eager panels, 1 lookahead panels
  *  GPX_OPT_POTRF_SWITCH    multi-launch schedule: -1 by size and batch (default), 0 no switch, k > 0: launches < k on
  *                          the lookahead schedule (flush every potrf_lazy, default 4 / by size), the rest eager (rounded
- *                          down to the launch after a flush) */
+ *                          down to the launch after a flush)
+ *  GPX_OPT_POTRF_SPLIT     panel row blocks per workgroup: -1 (default) split in 2 where the launch still fits the
+ *                          co-resident slots, 1 never split, 3 split only where the split launch fits one workgroup per CU */
 enum {
   GPX_OPT_RESERVED_0 = 0,
   GPX_OPT_SPIN_LIMIT = 1,
@@ -158,7 +160,8 @@ enum {
   GPX_OPT_POTRF_LAZY = 4,
   GPX_OPT_POTRF_MODE = 5,
   GPX_OPT_POTRF_SWITCH = 6,
-  GPX_OPT_COUNT = 7
+  GPX_OPT_POTRF_SPLIT = 7,
+  GPX_OPT_COUNT = 8
 };
 gpx_status gpx_set_option(gpx_handle h, int32_t option, int64_t value);
 gpx_status gpx_get_option(gpx_handle h, int32_t option, int64_t* value_host);

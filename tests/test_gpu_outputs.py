@@ -251,3 +251,47 @@ def test_reference_results_r3000_eight_outputs_own_parameters(engine):
     err = np.abs(sc.cpu().numpy() - sref).max()
     margin_guard(sref, err, "r3000 mean-of-8 logEI")
     check_argmax(int(bi.item()), sref, sc.cpu().numpy(), "r3000 mean-of-8 logEI")
+
+
+def test_per_output_entry_points_reject_invalid_arguments(engine):
+    """The C ABI's validation of the round-6 entry points: a bad parameter set names its problem, mixed input dimensions,
+    negative read-only strides and overlapping outputs, and a multi-output sweep over outputs of different n."""
+    import ctypes
+
+    from bayesianoptimizer_amd import GPXError
+    from bayesianoptimizer_amd._capi import KernelParamsC
+
+    n, d, T = 200, 3, 3
+    X, Y = problem(n, d, T, seed=19)
+    ps = output_params("rbf", d, T, seed=20)
+    with pytest.raises(GPXError, match="problem 1"):
+        engine.fit_outputs(t(X), t(Y), [ps[0], ps[1].replace(lengthscale=[0.3, -1.0, 0.2]), ps[2]])
+    with pytest.raises(ValueError):
+        engine.fit_outputs(t(X), t(Y), ps[:2])  # one parameter set per output
+    states = engine.fit_outputs(t(X), t(Y), ps)
+    lib, h = engine.lib, engine.handle
+    pcs = (KernelParamsC * T)(*[p.to_c(d) for p in ps])
+    pcs[2].d = 2  # mixed input dimensions
+    Lb, Wb, Db, Ab, Ib = states[0]._batch
+    nbytes = ctypes.c_size_t()
+    lib.gpx_fit_factor_batched_workspace_size(n, 1, T, ctypes.byref(nbytes))
+    ws = torch.empty(nbytes.value, dtype=torch.uint8, device=engine.device)
+    Xt, Yt = t(X), t(Y)
+    p_ = lambda v: ctypes.c_void_p(v.data_ptr())  # noqa: E731
+    npad = Lb.shape[1]
+
+    def call(pc, sx, sy, sk):
+        return lib.gpx_fit_factor_batched_params_f64(h, pc, T, n, p_(Xt), d, sx, p_(Yt), T, sy, 1, p_(Lb), npad, sk,
+                                                     p_(Db), Db.stride(0), p_(Ab), Ab.stride(0), p_(Ib), p_(ws),
+                                                     ws.numel())
+
+    assert call(pcs, 0, 1, Lb.stride(0)) != 0
+    assert "same input dimension" in lib.gpx_last_error(h).decode()
+    pcs[2].d = d
+    assert call(pcs, -1, 1, Lb.stride(0)) != 0      # negative read-only stride
+    assert call(pcs, 0, 1, 0) != 0                  # overlapping factors
+    assert call(pcs, 0, 1, Lb.stride(0)) == 0       # and the valid call goes through
+    X2, Y2 = problem(n + 5, d, 1, seed=21)
+    other = engine.fit_outputs(t(X2), t(Y2), ps[:1])
+    with pytest.raises(ValueError):
+        engine.acquire_multi([states[0], other[0]], t(np.random.default_rng(1).random((64, d))), "logei")
