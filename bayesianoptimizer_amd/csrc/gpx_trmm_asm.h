@@ -239,15 +239,16 @@ struct TileT {
 
   // One k-tile from LDS buffer CUR (see the file comment).  NEXT: a following k-tile exists (staged in the operands'
   // registers: written to the other buffer during S0, its substep-0 fragments read during S3); NEXT2: the tile after it
-  // exists (its global loads issued during S1 from descriptors rA / rB).  MM = false (wave-uniform): the same memory
-  // traffic without the MFMAs (a wave whose operand rows are all zero in this k-tile).
+  // exists (its global loads issued during S1 from descriptors rA / rB).  skip (wave-uniform, 0-4): the wave's first
+  // `skip` 16-row blocks have all-zero operand rows in this k-tile (a triangular operand's diagonal), so their MFMAs are
+  // left out (4: the same memory traffic without any MFMA).
   template <int CUR, bool NEXT, bool NEXT2>
-  __device__ __forceinline__ void ktile(rsrc_t rA, rsrc_t rB, bool MM = true) {
+  __device__ __forceinline__ void ktile(rsrc_t rA, rsrc_t rB, int skip = 0) {
     constexpr int NXT = CUR ^ 1;
     wait_lgkm<0>(f0);
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      if (MM) mm(f0, e);
+      if ((e >> 2) >= skip) mm(f0, e);
       if (e < 8) read_frag<CUR, 1>(f1, e);
       if (NEXT) {
         if (e == 7) wait_vm0(A, B);
@@ -262,7 +263,7 @@ struct TileT {
       wait_lgkm<0>(f1);
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      if (MM) mm(f1, e);
+      if ((e >> 2) >= skip) mm(f1, e);
       if (e < 8) read_frag<CUR, 2>(f0, e);
       if (NEXT2)
 #pragma unroll
@@ -271,14 +272,14 @@ struct TileT {
     wait_lgkm<0>(f0);
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      if (MM) mm(f0, e);
+      if ((e >> 2) >= skip) mm(f0, e);
       if (e < 8) read_frag<CUR, 3>(f1, e);
     }
     wait_lgkm<0>(f1);
     if (NEXT) asm volatile("s_barrier" ::: "memory");
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      if (MM) mm(f1, e);
+      if ((e >> 2) >= skip) mm(f1, e);
       if (NEXT && e < 8) read_frag<NXT, 0>(f0, e);
     }
   }
@@ -328,10 +329,10 @@ struct TileT {
     auto dB = [&](int kt) { return B.at(Bg, ldb, kt); };
     int k = 0;
     if (HEAD) {  // tiles 0-3 (their tiles after next exist: nk >= 6)
-      ktile<0, true, true>(dA(2), dB(2), !skip_head);
-      ktile<1, true, true>(dA(3), dB(3), !skip_head);
-      ktile<0, true, true>(dA(4), dB(4), !skip_head);
-      ktile<1, true, true>(dA(5), dB(5), !skip_head);
+      ktile<0, true, true>(dA(2), dB(2), skip_head ? 4 : 0);
+      ktile<1, true, true>(dA(3), dB(3), skip_head ? 4 : 0);
+      ktile<0, true, true>(dA(4), dB(4), skip_head ? 4 : 0);
+      ktile<1, true, true>(dA(5), dB(5), skip_head ? 4 : 0);
       k = 4;
     }
     const int kmain = TAIL ? nk - 4 : nk - 2;  // tiles [k, kmain) in the pair loop, each with a tile after next
@@ -340,11 +341,54 @@ struct TileT {
       ktile<1, true, true>(dA(k + 3), dB(k + 3));
     }
     if (TAIL) {
-      ktile<0, true, true>(dA(nk - 2), dB(nk - 2), !skip_tail);
-      ktile<1, true, true>(dA(nk - 1), dB(nk - 1), !skip_tail);
+      ktile<0, true, true>(dA(nk - 2), dB(nk - 2), skip_tail ? 4 : 0);
+      ktile<1, true, true>(dA(nk - 1), dB(nk - 1), skip_tail ? 4 : 0);
     }
-    ktile<0, true, false>(dA(0), dB(0), !(TAIL && skip_tail));
-    ktile<1, false, false>(dA(0), dB(0), !(TAIL && skip_tail));
+    ktile<0, true, false>(dA(0), dB(0), (TAIL && skip_tail) ? 4 : 0);
+    ktile<1, false, false>(dA(0), dB(0), (TAIL && skip_tail) ? 4 : 0);
+    // the last MFMAs' results are read by VALU code next: 24 wait states (cdna_hip_programming.md §5.7 item 2)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // run() for an upper-triangular A block row (A(m, k) = 0 for k > m + 128 (nk / 8 - 1)), nk a multiple of 8: the last
+  // 8 k-tiles are the diagonal 128-block, local k-tile j = 0..7, in which the waves of rows 0-63 skip their row blocks
+  // i < j (all of them for j >= 4) and the waves of rows 64-127 their row blocks i < j - 4.
+  __device__ void run_tri(const double* __restrict__ Ag, int64_t lda, const double* __restrict__ Bg, int64_t ldb, int nk,
+                          double* smem) {
+    const int w = threadIdx.x >> 6;
+    const int lo = __builtin_amdgcn_readfirstlane(w >> 1) == 0 ? 0 : 4;  // 4: rows 64-127
+    const unsigned lds0 = (unsigned)(uintptr_t)smem;
+    A.init(lds0, 0, (w >> 1) * 64, lda);
+    B.init(lds0, SB_OFF, (w & 1) * 64, ldb);
+#pragma unroll
+    for (int q = 0; q < NL; ++q) gload(A.at(Ag, lda, 0), B.at(Bg, ldb, 0), q);
+    wait_vm<0>(A, B);
+#pragma unroll
+    for (int q = 0; q < NW; ++q) lwrite<0>(q);
+#pragma unroll
+    for (int q = 0; q < NL; ++q) gload(A.at(Ag, lda, 1), B.at(Bg, ldb, 1), q);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+    for (int q = 0; q < 8; ++q) read_frag<0, 0>(f0, q);
+    auto dA = [&](int kt) { return A.at(Ag, lda, kt); };
+    auto dB = [&](int kt) { return B.at(Bg, ldb, kt); };
+    // the wave's zero row blocks in local k-tile j: min(max(j - lo, 0), 4)
+    auto sk = [&](int j) { const int v = j - lo; return v < 0 ? 0 : (v > 4 ? 4 : v); };
+    const int kd = nk - 8;  // first k-tile of the diagonal block
+    for (int k = 0; k < kd; k += 2) {
+      ktile<0, true, true>(dA(k + 2), dB(k + 2));
+      ktile<1, true, true>(dA(k + 3), dB(k + 3));
+    }
+    ktile<0, true, true>(dA(kd + 2), dB(kd + 2), sk(0));
+    ktile<1, true, true>(dA(kd + 3), dB(kd + 3), sk(1));
+    ktile<0, true, true>(dA(kd + 4), dB(kd + 4), sk(2));
+    ktile<1, true, true>(dA(kd + 5), dB(kd + 5), sk(3));
+    ktile<0, true, true>(dA(kd + 6), dB(kd + 6), sk(4));
+    ktile<1, true, true>(dA(kd + 7), dB(kd + 7), sk(5));
+    ktile<0, true, false>(dA(0), dB(0), sk(6));
+    ktile<1, false, false>(dA(0), dB(0), sk(7));
     // the last MFMAs' results are read by VALU code next: 24 wait states (cdna_hip_programming.md §5.7 item 2)
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -352,14 +396,15 @@ struct TileT {
   }
 };
 
-// The sweep product's tile: both operands k-major, the triangular W's zero 64-block skipped by the waves of rows 0-63.
+// The sweep product's tile: both operands k-major; for the triangular W (zero_tail: nk a multiple of 8) the zero 16 x 16
+// blocks of the diagonal 128-block are skipped (run_tri: the waves of rows 0-63 / 64-127 form 10 / 26 of their 32 row-block
+// x k-tile products there, against 16 / 32 when only the zero 64-block was skipped).
 struct Tile : TileT<true, true> {
   __device__ void run(const double* __restrict__ Ag, int64_t lda, const double* __restrict__ Bg, int64_t ldb, int nk,
                       double* smem, bool zero_tail) {
     zero();
-    const bool skip = zero_tail && __builtin_amdgcn_readfirstlane(threadIdx.x >> 7) == 0;
     if (zero_tail)
-      TileT<true, true>::run<false, true>(Ag, lda, Bg, ldb, nk, smem, false, skip);
+      TileT<true, true>::run_tri(Ag, lda, Bg, ldb, nk, smem);
     else
       TileT<true, true>::run<false, false>(Ag, lda, Bg, ldb, nk, smem);
   }
