@@ -9,6 +9,8 @@
 //   A5  A1 with workgroups 256..511 (the second slot of every CU in the first round) sleeping ~half a tile first, so the
 //       two tiles of a CU never load / store at the same time (the stagger then persists)
 //   A6  A5 with a quarter-tile sleep
+//   A7  A1 with the panels read in place from a factor-shaped buffer (row stride 16384 doubles, as the library's flush
+//       reads L from A), against A1's packed panels (row stride K)
 // F0 / A3 must agree bit for bit, and A1 / A2 / A4 among themselves (the seeded chain rounds differently from C - acc).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form=1 -I../bayesianoptimizer_amd/csrc
 //        flush_asm_bench.hip -o flush_asm_bench
@@ -52,7 +54,7 @@ __device__ __forceinline__ void xcd_tile(int t, int T, int M, int& I, int& J) {
 template <int V>
 __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2)))
 flush_v(double* __restrict__ Cm, int64_t ldc, const double* __restrict__ L, const double* __restrict__ LT, int64_t m,
-        int K, int M) {
+        int K, int M, const double* __restrict__ LW = nullptr, int64_t ldw = 0) {
   __shared__ __attribute__((aligned(16))) double lds[trmm_asm::LDS_BYTES / 8];
   const int T = M * (M + 1) / 2;
   int I, J;
@@ -90,9 +92,9 @@ flush_v(double* __restrict__ Cm, int64_t ldc, const double* __restrict__ L, cons
   } else {
     constexpr bool KM = V == 2;
     trmm_asm::TileT<KM, KM, true> tl;
-    const double* A = KM ? LT + (int64_t)I * 128 : L + (int64_t)I * 128 * K;
-    const double* B = KM ? LT + (int64_t)J * 128 : L + (int64_t)J * 128 * K;
-    const int64_t ld = KM ? m : K;
+    const double* A = KM ? LT + (int64_t)I * 128 : (V == 7 ? LW + (int64_t)I * 128 * ldw : L + (int64_t)I * 128 * K);
+    const double* B = KM ? LT + (int64_t)J * 128 : (V == 7 ? LW + (int64_t)J * 128 * ldw : L + (int64_t)J * 128 * K);
+    const int64_t ld = KM ? m : (V == 7 ? ldw : K);
     auto rc = trmm_asm::rsrc_of(C);
     tl.template run_after<false, false, 64>(A, ld, B, ld, K / 16, lds, [&] {
       const int v0 = (int)(((int64_t)MT::row_of(0, 0) * ldc + MT::col_of(0)) * 8);
@@ -121,10 +123,11 @@ flush_v(double* __restrict__ Cm, int64_t ldc, const double* __restrict__ L, cons
 
 struct Bufs {
   int m, K, M, tiles;
-  double *C, *C0, *L, *LT;
+  double *C, *C0, *L, *LT, *LW;
+  int64_t ldw;
 };
 static Bufs make(int m, int K) {
-  Bufs b{m, K, m / 128, (m / 128) * (m / 128 + 1) / 2, nullptr, nullptr, nullptr, nullptr};
+  Bufs b{m, K, m / 128, (m / 128) * (m / 128 + 1) / 2, nullptr, nullptr, nullptr, nullptr, nullptr, 16384};
   std::vector<double> hL((size_t)m * K), hLT((size_t)m * K), hC((size_t)m * m);
   srand(5);
   for (int i = 0; i < m; ++i)
@@ -137,6 +140,8 @@ static Bufs make(int m, int K) {
   CK(hipMemcpy(b.L, hL.data(), hL.size() * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(b.LT, hLT.data(), hLT.size() * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(b.C0, hC.data(), hC.size() * 8, hipMemcpyHostToDevice));
+  CK(hipMalloc(&b.LW, (size_t)m * b.ldw * 8));
+  CK(hipMemcpy2D(b.LW, b.ldw * 8, b.L, (size_t)K * 8, (size_t)K * 8, m, hipMemcpyDeviceToDevice));
   return b;
 }
 static void run(const Bufs& b, int v) {
@@ -147,15 +152,17 @@ static void run(const Bufs& b, int v) {
     case 3: flush_v<3><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
     case 4: flush_v<4><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
     case 5: flush_v<5><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
-    default: flush_v<6><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
+    case 6: flush_v<6><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
+    default: flush_v<7><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M, b.LW, b.ldw); break;
   }
 }
 
 int main(int argc, char** argv) {
   const int m = argc > 1 ? atoi(argv[1]) : 15872, K = argc > 2 ? atoi(argv[2]) : 512;
   const char* names[] = {"F0 MfmaTile C-acc", "A1 asm seeded", "A2 asm seeded k-major", "A3 asm C-acc",
-                         "A4 A1 row-major order", "A5 A1 + half-tile stagger", "A6 A1 + quarter stagger"};
-  constexpr int NV = 7;
+                         "A4 A1 row-major order", "A5 A1 + half-tile stagger", "A6 A1 + quarter stagger",
+                         "A7 A1 panels in place"};
+  constexpr int NV = 8;
   {  // bit-for-bit checks at a small size
     Bufs b = make(2048, K);
     const size_t mm = (size_t)b.m * b.m;
@@ -171,8 +178,9 @@ int main(int argc, char** argv) {
       for (size_t q = 0; q < mm; ++q) bad += out[x][q] != out[y][q];
       return bad;
     };
-    printf("m=%d K=%d: mismatches F0-A3 %zu, A1-A2 %zu, A1-A4 %zu, A1-A5 %zu, A1-A6 %zu (F0-A1 %zu: the seeded chain rounds "
-           "differently)\n", b.m, K, diff(0, 3), diff(1, 2), diff(1, 4), diff(1, 5), diff(1, 6), diff(0, 1));
+    printf("m=%d K=%d: mismatches F0-A3 %zu, A1-A2 %zu, A1-A4 %zu, A1-A5 %zu, A1-A6 %zu, A1-A7 %zu (F0-A1 %zu: the seeded "
+           "chain rounds differently)\n", b.m, K, diff(0, 3), diff(1, 2), diff(1, 4), diff(1, 5), diff(1, 6), diff(1, 7),
+           diff(0, 1));
   }
   Bufs b = make(m, K);
   hipEvent_t e0, e1;
