@@ -11,6 +11,7 @@
 //   A6  A5 with a quarter-tile sleep
 //   A7  A1 with the panels read in place from a factor-shaped buffer (row stride 16384 doubles, as the library's flush
 //       reads L from A), against A1's packed panels (row stride K)
+//   A8  A1 storing C as the library does: write-through (sc1) 16-byte pairs (gpx_potrf.hip store_block_pairs_sc1)
 // F0 / A3 must agree bit for bit, and A1 / A2 / A4 among themselves (the seeded chain rounds differently from C - acc).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form=1 -I../bayesianoptimizer_amd/csrc
 //        flush_asm_bench.hip -o flush_asm_bench
@@ -49,6 +50,20 @@ __device__ __forceinline__ void xcd_tile(int t, int T, int M, int& I, int& J) {
     }
   }
   I = J = 0;
+}
+
+// gpx_potrf.hip's write-through pair store (copied: that file is not included here)
+__device__ __forceinline__ double swap_adjacent(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(u & 0xffffffffull), 0xB1, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), 0xB1, 0xf, 0xf, false);
+  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ void st2(trmm_asm::rsrc_t r, int off, double a, double b) {
+  const unsigned long long x = __double_as_longlong(a), y = __double_as_longlong(b);
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const u4 v = {(unsigned)x, (unsigned)(x >> 32), (unsigned)y, (unsigned)(y >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
 }
 
 template <int V>
@@ -113,6 +128,23 @@ flush_v(double* __restrict__ Cm, int64_t ldc, const double* __restrict__ L, cons
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = tl.acc[i][j];
   }
+  if constexpr (V == 8) {
+    const auto rc = trmm_asm::rsrc_of(C);
+    const bool even = (threadIdx.x & 1) == 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const d4& v = acc[i][j];
+        const double x0 = swap_adjacent(even ? v[2] : v[0]);
+        const double x1 = swap_adjacent(even ? v[3] : v[1]);
+        const int col = MT::col_of(j) & ~1;
+        const int ra = MT::row_of(i, even ? 0 : 2), rb = MT::row_of(i, even ? 1 : 3);
+        st2(rc, (int)(((int64_t)ra * ldc + col) * 8), even ? v[0] : x0, even ? x0 : v[2]);
+        st2(rc, (int)(((int64_t)rb * ldc + col) * 8), even ? v[1] : x1, even ? x1 : v[3]);
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -153,7 +185,8 @@ static void run(const Bufs& b, int v) {
     case 4: flush_v<4><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
     case 5: flush_v<5><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
     case 6: flush_v<6><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
-    default: flush_v<7><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M, b.LW, b.ldw); break;
+    case 7: flush_v<7><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M, b.LW, b.ldw); break;
+    default: flush_v<8><<<b.tiles, WG>>>(b.C, b.m, b.L, b.LT, b.m, b.K, b.M); break;
   }
 }
 
@@ -161,8 +194,8 @@ int main(int argc, char** argv) {
   const int m = argc > 1 ? atoi(argv[1]) : 15872, K = argc > 2 ? atoi(argv[2]) : 512;
   const char* names[] = {"F0 MfmaTile C-acc", "A1 asm seeded", "A2 asm seeded k-major", "A3 asm C-acc",
                          "A4 A1 row-major order", "A5 A1 + half-tile stagger", "A6 A1 + quarter stagger",
-                         "A7 A1 panels in place"};
-  constexpr int NV = 8;
+                         "A7 A1 panels in place", "A8 A1 write-through pairs"};
+  constexpr int NV = 9;
   {  // bit-for-bit checks at a small size
     Bufs b = make(2048, K);
     const size_t mm = (size_t)b.m * b.m;
@@ -178,9 +211,9 @@ int main(int argc, char** argv) {
       for (size_t q = 0; q < mm; ++q) bad += out[x][q] != out[y][q];
       return bad;
     };
-    printf("m=%d K=%d: mismatches F0-A3 %zu, A1-A2 %zu, A1-A4 %zu, A1-A5 %zu, A1-A6 %zu, A1-A7 %zu (F0-A1 %zu: the seeded "
-           "chain rounds differently)\n", b.m, K, diff(0, 3), diff(1, 2), diff(1, 4), diff(1, 5), diff(1, 6), diff(1, 7),
-           diff(0, 1));
+    printf("m=%d K=%d: mismatches F0-A3 %zu, A1-A2 %zu, A1-A4 %zu, A1-A5 %zu, A1-A6 %zu, A1-A7 %zu, A1-A8 %zu (F0-A1 %zu: the "
+           "seeded chain rounds differently)\n", b.m, K, diff(0, 3), diff(1, 2), diff(1, 4), diff(1, 5), diff(1, 6),
+           diff(1, 7), diff(1, 8), diff(0, 1));
   }
   Bufs b = make(m, K);
   hipEvent_t e0, e1;
