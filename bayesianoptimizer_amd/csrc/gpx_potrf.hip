@@ -921,10 +921,15 @@ static int potrf_mode(const Context* ctx, int nblk, int batch) {
   return nblk > 64 || batched_lookahead(nblk, batch) ? 1 : 0;
 }
 
-// A single fit of 64 blocks runs its first launches (c < 9) on the lookahead schedule with a flush every 4 columns and
-// switches to the eager schedule right after the flush at c = 8 (the eager launch c then applies column c - 1 to the
-// panels and the trailing matrix: every column is applied exactly once).  The early launches are bound by the eager
-// schedule's C traffic (launches 1-4: 39-42 us against ~17 us of panel chain, profiles/r04_potrf_launches_4096.log):
+// A single fit of 64 blocks runs its first launches (c < 25) on the lookahead schedule with a flush every 3 columns and
+// switches to the eager schedule right after the flush at c = 24 (the eager launch c then applies column c - 1 to the
+// panels and the trailing matrix: every column is applied exactly once).  Round 6 (profiles/r06_potrf_switch_ab.log, one
+// process, alternating arms, alpha bit-identical): switch 25 / g 3 1.5472 vs 1.5666 ms for round 5's switch 9 / g 4
+// (1.5542 vs 1.5670 in a second sweep; 22 / 3 1.5547, 28 / 3 1.5554, 31 / 3 1.5644, 25 / 2 1.5615, 25 / 4 1.5597,
+// 25 / 6 1.5539, 33 / 2 1.5849): in launches 9-24 the eager schedule moved the whole trailing matrix every column and
+// the panel waited on that traffic (profiles/r06_potrf_steps_4096.log: pre-update 17-22 us there against ~6 in the tail).
+// Round 4 introduced the switch: the early launches are bound by the eager schedule's C traffic (launches 1-4: 39-42 us
+// against ~17 us of panel chain, profiles/r04_potrf_launches_4096.log):
 // update 1.617 -> 1.596 ms at n = 4096 (profiles/r04_potrf_hybrid_ab.log; switch at c = 5 / 9 / 13 / 17 / 25 / 33 with
 // g = 4: 1.596 / 1.596-1.602 / 1.602 / 1.616 / 1.618 / 1.630 vs 1.616-1.619; g = 2 / 8 no better; the kept form 1.599 vs
 // 1.616).  Smaller fits keep the eager schedule throughout: the same switch at n = 2048 / 3072 / 3584 gave 0.683 / 1.058
@@ -934,7 +939,7 @@ static int potrf_mode(const Context* ctx, int nblk, int batch) {
 // launches' panel chain is the shorter one (profiles/r04_potrf_eager_tail_ab.log: n = 8192 5.832 -> 5.720 ms with the
 // last 32, 5.811 -> 5.748 with 24, 5.796 -> 5.731 with 48; n = 16384 29.865 -> 29.715 with 32).
 constexpr int kEagerTail = 32;
-constexpr int kSwitchLazy = 4;  // the flush interval before the switch (the switch launch follows a flush launch)
+constexpr int kSwitchLazy = 3;  // the flush interval before the switch (the switch launch follows a flush launch)
 // flush interval of the launches before the switch: mode 0 (eager after it) kSwitchLazy or GPX_OPT_POTRF_LAZY when the
 // switch is set by option; mode 1 (lookahead before it) the schedule's own interval g
 static int early_lazy(const Context* ctx, int mode, int g) {
@@ -956,7 +961,7 @@ static int potrf_switch(const Context* ctx, int nblk, int batch, int mode, int g
     if (!batched_lookahead(nblk, batch)) return 0;
     return ((nblk - (batch >= 4 ? 16 : 17)) / g) * g + 1;
   }
-  if (mode == 0) return nblk == 64 ? 9 : 0;
+  if (mode == 0) return nblk == 64 ? 25 : 0;
   if (nblk - kEagerTail < g + 1) return 0;
   return ((nblk - kEagerTail - 1) / g) * g + 1;
 }
