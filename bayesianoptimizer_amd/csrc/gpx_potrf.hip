@@ -913,7 +913,11 @@ static int potrf_lazy(const Context* ctx, int nblk, int batch) {
   if (ctx->potrf_lazy > 0) return ctx->potrf_lazy;
   if (batched_lookahead(nblk, batch)) return batch >= 4 ? 6 : 4;
   if (batch >= 2 && nblk > 64) return nblk > 100 ? 8 : 6;
-  return nblk > 128 ? 8 : (nblk > 100 ? 6 : (nblk > 64 ? 4 : 1));
+  // round 6 (profiles/r06_potrf_n16384_schedule_ab.log, one process, alternating arms): n = 16384 flushes every 12
+  // columns (K = 768), eager for the last ~51: 28.11-28.16 vs 28.56-28.63 ms for 8 / the last 39 (10: 28.30-28.35, 13:
+  // 28.31, 14: 28.21, 16: 28.39); n = 12288 (g = 10 / 12: 13.95 / 14.03 vs 13.98) and n = 8192 (g = 8 / 10 / 12: 5.53 /
+  // 5.58 / 5.67 vs 5.54) keep theirs
+  return nblk > 192 ? 12 : (nblk > 128 ? 8 : (nblk > 100 ? 6 : (nblk > 64 ? 4 : 1)));
 }
 
 static int potrf_mode(const Context* ctx, int nblk, int batch) {
@@ -962,8 +966,9 @@ static int potrf_switch(const Context* ctx, int nblk, int batch, int mode, int g
     return ((nblk - (batch >= 4 ? 16 : 17)) / g) * g + 1;
   }
   if (mode == 0) return nblk == 64 ? 25 : 0;
-  if (nblk - kEagerTail < g + 1) return 0;
-  return ((nblk - kEagerTail - 1) / g) * g + 1;
+  const int tail = g >= 12 ? 48 : kEagerTail;  // (n = 16384, g = 12: the eager part from c = 205)
+  if (nblk - tail < g + 1) return 0;
+  return ((nblk - tail - 1) / g) * g + 1;
 }
 
 // The plan of every launch c < cend (flush launches: c >= 1 and at least one interval after the previous flush);
