@@ -932,7 +932,8 @@ static int potrf_mode(const Context* ctx, int nblk, int batch) {
 // (1.5542 vs 1.5670 in a second sweep; 22 / 3 1.5547, 28 / 3 1.5554, 31 / 3 1.5644, 25 / 2 1.5615, 25 / 4 1.5597,
 // 25 / 6 1.5539, 33 / 2 1.5849; the same start at n = 3072 / 3584 / 5120 measured neutral or slower,
 // profiles/r06_potrf_midn_schedule_ab.log): in launches 9-24 the eager schedule moved the whole trailing matrix every
-// column and the panel waited on that traffic (profiles/r06_potrf_steps_4096_switch9.log: pre-update 17-22 us there, ~6 in the tail).
+// column and the panel waited on that traffic (profiles/r06_potrf_steps_4096_switch9.log: pre-update 17-22 us there,
+// ~6 in the tail).
 // Round 4 introduced the switch: the early launches are bound by the eager schedule's C traffic (launches 1-4: 39-42 us
 // against ~17 us of panel chain, profiles/r04_potrf_launches_4096.log):
 // update 1.617 -> 1.596 ms at n = 4096 (profiles/r04_potrf_hybrid_ab.log; switch at c = 5 / 9 / 13 / 17 / 25 / 33 with
