@@ -148,7 +148,7 @@ size_t gpx_acq_params_size(void);
  *  GPX_OPT_POTRF_LAZY      multi-launch schedule: 0 by size and batch (default), else flush the trailing update every g columns
  *  GPX_OPT_POTRF_MODE      multi-launch schedule: -1 by size and batch (default), 0 eager panels, 1 lookahead panels
  *  GPX_OPT_POTRF_SWITCH    multi-launch schedule: -1 by size and batch (default), 0 no switch, k > 0: launches < k on
- *                          the lookahead schedule (flush every potrf_lazy, default 4 / by size), the rest eager (rounded
+ *                          the lookahead schedule (flush every potrf_lazy, default 3 / by size), the rest eager (rounded
  *                          down to the launch after a flush)
  *  GPX_OPT_POTRF_SPLIT     panel row blocks per workgroup: -1 (default) split in 2 where the launch still fits the
  *                          co-resident slots, 1 never split, 3 split only where the split launch fits one workgroup per CU */
