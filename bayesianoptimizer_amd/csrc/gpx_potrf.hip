@@ -905,8 +905,12 @@ __global__ void __launch_bounds__(WG) potrf_dinv_kernel(double* __restrict__ A, 
 // The handle options GPX_OPT_POTRF_LAZY / GPX_OPT_POTRF_MODE override.  Flushing every second launch only in the early,
 // trailing-bound launches and panel-wave priority were measured neutral (DESIGN_HISTORY.md, items 14 and the prio knob)
 // and are not offered.  Trailing tiles are dealt to the XCDs in 8 x 8 super-block chunks (trail_tile xmap = 1).
+// Round 6 (profiles/r06_small_batched_schedule_ab.log, one process, alternating arms): batches of 8 take the lookahead
+// schedule (g = 6) from 24 blocks on as well - the drop-in's 8-output fits below the SVGP threshold (n <= 3000) - :
+// n = 1536 / 2048 / 2560 0.822 -> 0.767, 1.360 -> 1.248, 2.153 -> 1.908 ms (eager for the last 16 columns only from
+// 40 blocks on: 2048 with it 1.262, 2560 without it 1.927); 16 blocks (n = 1024) and B = 4 at 32 blocks stay eager.
 static bool batched_lookahead(int nblk, int batch) {
-  return nblk <= 64 && ((batch >= 2 && nblk >= 56) || (batch >= 4 && nblk >= 48));
+  return nblk <= 64 && ((batch >= 2 && nblk >= 56) || (batch >= 4 && nblk >= 48) || (batch >= 8 && nblk >= 24));
 }
 
 static int potrf_lazy(const Context* ctx, int nblk, int batch) {
@@ -964,7 +968,7 @@ static int potrf_switch(const Context* ctx, int nblk, int batch, int mode, int g
     // 3.195 -> 3.149 ms with the switch at 49, 3.153 at 37, 3.219 at 25; profiles/r05_potrf_schedules.log): the
     // launch after the last flush at or before nblk - 16 for B >= 4 (g = 6: 49 vs 43 3.118 vs 3.135 ms in a sweep, 3.155 vs 3.165 B = 4 and 5.353 vs 5.362 B = 8 in an A/B,
     // profiles/r05_potrf_batched_switch_ab.log), one launch earlier for B = 2 (g = 4: 45; 49 measured 2.138 vs 2.133)
-    if (!batched_lookahead(nblk, batch)) return 0;
+    if (!batched_lookahead(nblk, batch) || nblk < 40) return 0;
     return ((nblk - (batch >= 4 ? 16 : 17)) / g) * g + 1;
   }
   if (mode == 0) return nblk == 64 ? 25 : 0;
